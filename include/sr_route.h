@@ -1,0 +1,123 @@
+/*
+ * sr_route.h — C ABI of the MI355X-native statsd-router hot path.
+ *
+ * The reference (hulu/statsd-router) has no plugin or FFI API: its hot path is the libev
+ * callback `udp_read_cb` (sr-main.c:149-191), which frames one datagram and, per '\n'-terminated
+ * line, calls `process_data_line` (sr-main.c:137-147) -> `hash` (sr-main.c:120-134) ->
+ * `find_downstream` (sr-main.c:86-117) -> `push_to_downstream` (sr-main.c:73-83).
+ * This header replaces the per-line calls with one call per BATCH of framed datagrams:
+ * the GPU classifies every line (length gate, ':' presence, sdbm name hash, consistent-hash
+ * shard pick) and returns one record per line in input order. The host caller keeps the
+ * reference's side effects: it walks the records and does push_to_downstream, the WARN log
+ * lines (exact reference text) and the dead-downstream buffer drop (sr-main.c:106).
+ *
+ * Conventions (mirroring the reference):
+ *   - every function returns 0 or a negative errno value; nothing aborts;
+ *   - a context is not thread-safe: use one per data thread / HIP stream, like one libev loop
+ *     per thread (sr-main.c:237-308);
+ *   - the alive bitmap is a snapshot (the reference reads the `alive:1` bit of
+ *     ds_health_client_s (sr-types.h:25) racily per line; a per-batch snapshot is a valid
+ *     linearisation of that).
+ *
+ * No torch or HIP types appear in the signatures: device pointers are plain pointers and the
+ * stream is an opaque `void *` (a hipStream_t).
+ */
+#ifndef SR_ROUTE_H
+#define SR_ROUTE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- constants of the reference contract ------------------------------------------------ */
+#define SR_DATA_BUF_SIZE        4096u  /* sr-main.h:46: recv buffer; recv() reads at most 4095 B */
+#define SR_MAX_DATAGRAM         (SR_DATA_BUF_SIZE - 1u)   /* sr-main.c:163 */
+#define SR_DOWNSTREAM_BUF_SIZE  1450u  /* sr-types.h:30: a valid line is shorter than this      */
+#define SR_MIN_LINE_LENGTH      6u     /* sr-main.c:180: `line_length > 5`                        */
+#define SR_MAX_LINE_LENGTH      (SR_DOWNSTREAM_BUF_SIZE - 1u)  /* sr-main.c:180: `< 1450`         */
+#define SR_MAX_DOWNSTREAMS      65533u /* shard ids must fit below the SR_ROUTE_* codes         */
+
+/* ---- per-line verdicts -------------------------------------------------------------------- */
+enum sr_verdict {
+    SR_VALID          = 0, /* routed: process_data_line -> find_downstream -> push (sr-main.c:103) */
+    SR_INVALID_LENGTH = 1, /* WARN "udp_read_cb: invalid length %d of metric %.*s" (sr-main.c:184)  */
+    SR_INVALID_FORMAT = 2, /* WARN "process_data_line: invalid metric %s" (sr-main.c:142)            */
+    SR_ALL_DEAD       = 3  /* WARN "find_downstream: all downstreams are dead" (sr-main.c:115)       */
+};
+
+/* `route` field: the shard id (0..n_downstreams-1) for SR_VALID, else one of these codes. */
+#define SR_ROUTE_INVALID_LENGTH 0xFFFDu
+#define SR_ROUTE_INVALID_FORMAT 0xFFFEu
+#define SR_ROUTE_ALL_DEAD       0xFFFFu
+
+/* One record per '\n'-terminated line, in input order. 8 bytes, little-endian, no padding. */
+typedef struct sr_record {
+    uint32_t offset; /* byte offset of the line's first byte in the batch                  */
+    uint16_t length; /* bytes including the '\n' (saturates at 0xFFFF; lines > 4096 B only  */
+                     /* occur when the caller breaks the framing contract)                  */
+    uint16_t route;  /* shard id, or SR_ROUTE_*                                             */
+} sr_record;
+
+static inline int sr_record_verdict(const sr_record *r) {
+    return r->route < SR_ROUTE_INVALID_LENGTH ? SR_VALID : (int)(r->route - 0xFFFCu);
+}
+
+/* ---- host-side framing (no GPU) ----------------------------------------------------------- */
+/* Frame one received datagram exactly as udp_read_cb does (sr-main.c:163-173): keep at most
+ * SR_MAX_DATAGRAM bytes (the recv() cap) and append '\n' if the last kept byte is not one.
+ * Writes at most len+1 (<= 4096) bytes to dst; returns the framed length (0 for an empty datagram).
+ * dst must not overlap src. */
+size_t sr_frame_datagram(uint8_t *dst, const uint8_t *src, size_t len);
+
+/* Frame `count` datagrams back to back into dst (capacity dst_cap). Returns the total framed
+ * length, or (size_t)-1 if dst_cap is too small. */
+size_t sr_frame_datagrams(uint8_t *dst, size_t dst_cap, const uint8_t *const *dgrams,
+                          const size_t *lens, size_t count);
+
+/* ---- context -------------------------------------------------------------------------------- */
+typedef struct sr_ctx sr_ctx;
+
+/* Open a context on HIP device `device` for batches of at most max_batch_bytes framed bytes and
+ * n_downstreams shards (the order of the `downstream=` list in statsd-router.conf, sr-init.c:61-121).
+ * All downstreams start alive. Allocates device buffers and a HIP stream.
+ * Returns 0, -EINVAL, -ENODEV or -ENOMEM. */
+int sr_open(sr_ctx **ctx, int device, size_t max_batch_bytes, uint32_t n_downstreams);
+
+/* Snapshot of the health checker's alive bits (sr-health-client.c:15-18,37-40):
+ * bit k of alive_bitmap[k/64] = downstream k alive. ceil(n_downstreams/64) words. */
+int sr_set_alive(sr_ctx *ctx, const uint64_t *alive_bitmap);
+
+/* Enqueue work on `stream` (a hipStream_t) instead of the context's own stream (NULL restores it). */
+int sr_set_stream(sr_ctx *ctx, void *stream);
+
+/* Host-memory batch: copy `bytes` (concatenated framed datagrams; the last byte must be '\n'
+ * unless nbytes == 0) to the device, classify every line, copy min(n, max_records) records (and,
+ * if hashes != NULL, the 64-bit sdbm name hashes; 0 for invalid lines) back, and synchronise.
+ * *n_records = number of lines n. Returns 0, or -ENOSPC if n > max_records (the first
+ * max_records records are still valid), -EINVAL, -EIO. */
+int sr_route_batch(sr_ctx *ctx, const uint8_t *bytes, size_t nbytes, sr_record *out,
+                   size_t max_records, size_t *n_records, uint64_t *hashes);
+
+/* Device-resident batch (asynchronous, enqueued on the context's stream): d_bytes, d_out,
+ * d_hashes (may be NULL) and d_n_records are device pointers. Lines past max_records are counted
+ * but not written; the line count is stored to *d_n_records when the work completes.
+ * The input buffer needs no padding. Returns 0 or -EINVAL / -EIO (launch failure). */
+int sr_route_device(sr_ctx *ctx, const uint8_t *d_bytes, size_t nbytes, sr_record *d_out,
+                    size_t max_records, uint64_t *d_hashes, uint64_t *d_n_records);
+
+/* Wait for all work enqueued by this context. */
+int sr_sync(sr_ctx *ctx);
+
+void sr_close(sr_ctx *ctx);
+
+/* Version / build information string (static storage). */
+const char *sr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SR_ROUTE_H */

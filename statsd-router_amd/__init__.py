@@ -1,0 +1,247 @@
+"""statsd-router_amd — MI355X-native statsd-router hot path.
+
+Python view of the C ABI in ``include/sr_route.h`` (ctypes; the product is the C library
+``lib/libsr_route.so`` built from ``csrc/sr_route.hip``). The reference has no Python API; this
+module exists so tests and ``bench.py`` can drive the same C entry points a C host (the router's
+``udp_read_cb`` replacement) calls. Names follow the reference's domain: datagrams, lines,
+downstreams (shards), the alive bitmap.
+
+Loading is strict: if ``libsr_route.so`` is missing or lacks a symbol, importing raises. There is
+no CPU fallback of the hot path anywhere in this package.
+
+Import with ``importlib.import_module("statsd-router_amd")`` (the directory name has a hyphen).
+"""
+from __future__ import annotations
+
+import ctypes
+import errno
+import os
+from dataclasses import dataclass
+from typing import Iterable, Sequence
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+ROUTE_LIB = os.path.join(LIB_DIR, "libsr_route.so")
+GEN_LIB = os.path.join(LIB_DIR, "libsr_gen.so")
+HEADER = os.path.join(REPO_DIR, "include", "sr_route.h")
+
+# ---- constants mirrored from include/sr_route.h (checked against the header by tests) --------
+SR_DATA_BUF_SIZE = 4096
+SR_MAX_DATAGRAM = 4095
+SR_DOWNSTREAM_BUF_SIZE = 1450
+SR_MIN_LINE_LENGTH = 6
+SR_MAX_LINE_LENGTH = 1449
+SR_MAX_DOWNSTREAMS = 65533
+SR_VALID, SR_INVALID_LENGTH, SR_INVALID_FORMAT, SR_ALL_DEAD = 0, 1, 2, 3
+SR_ROUTE_INVALID_LENGTH = 0xFFFD
+SR_ROUTE_INVALID_FORMAT = 0xFFFE
+SR_ROUTE_ALL_DEAD = 0xFFFF
+
+RECORD_DTYPE = np.dtype([("offset", "<u4"), ("length", "<u2"), ("route", "<u2")])
+assert RECORD_DTYPE.itemsize == 8
+
+# every function the header declares (tests check the library exports exactly these)
+ABI_FUNCTIONS = (
+    "sr_frame_datagram", "sr_frame_datagrams", "sr_open", "sr_set_alive", "sr_set_stream",
+    "sr_route_batch", "sr_route_device", "sr_sync", "sr_close", "sr_version",
+)
+
+
+class SrError(OSError):
+    """A negative errno returned by the C ABI."""
+
+
+def _check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise SrError(-rc, f"{what}: {os.strerror(-rc)}")
+    return rc
+
+
+def verdicts(routes: np.ndarray) -> np.ndarray:
+    """Map the record ``route`` field to sr_verdict values (sr_record_verdict in the header)."""
+    r = np.asarray(routes, dtype=np.uint16)
+    v = np.zeros(r.shape, dtype=np.uint8)
+    bad = r >= SR_ROUTE_INVALID_LENGTH
+    v[bad] = (r[bad].astype(np.int32) - 0xFFFC).astype(np.uint8)
+    return v
+
+
+def _load_route_lib() -> ctypes.CDLL:
+    if not os.path.exists(ROUTE_LIB):
+        raise ImportError(
+            f"{ROUTE_LIB} is missing: build it with __graft_entry__.build() or `make -C statsd-router_amd`"
+        )
+    lib = ctypes.CDLL(ROUTE_LIB)
+    c_size_p = ctypes.POINTER(ctypes.c_size_t)
+    u64p = ctypes.POINTER(ctypes.c_uint64)
+    vp = ctypes.c_void_p
+    sig = {
+        "sr_frame_datagram": (ctypes.c_size_t, [vp, vp, ctypes.c_size_t]),
+        "sr_frame_datagrams": (ctypes.c_size_t, [vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t]),
+        "sr_open": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_size_t, ctypes.c_uint32]),
+        "sr_set_alive": (ctypes.c_int, [vp, u64p]),
+        "sr_set_stream": (ctypes.c_int, [vp, vp]),
+        "sr_route_batch": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, c_size_p, vp]),
+        "sr_route_device": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp, vp]),
+        "sr_sync": (ctypes.c_int, [vp]),
+        "sr_close": (None, [vp]),
+        "sr_version": (ctypes.c_char_p, []),
+    }
+    for name in ABI_FUNCTIONS:
+        fn = getattr(lib, name)  # raises AttributeError if the export is missing
+        fn.restype, fn.argtypes = sig[name]
+    return lib
+
+
+_LIB: ctypes.CDLL | None = None
+_GEN: ctypes.CDLL | None = None
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        _LIB = _load_route_lib()
+    return _LIB
+
+
+def gen_lib() -> ctypes.CDLL:
+    global _GEN
+    if _GEN is None:
+        if not os.path.exists(GEN_LIB):
+            raise ImportError(f"{GEN_LIB} is missing: build with __graft_entry__.build()")
+        g = ctypes.CDLL(GEN_LIB)
+        g.sr_gen_stream.restype = ctypes.c_size_t
+        g.sr_gen_stream.argtypes = [
+            ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_double,
+            ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_size_t,
+            ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t),
+        ]
+        _GEN = g
+    return _GEN
+
+
+# ---- framing (host, no GPU) -----------------------------------------------------------------
+def frame_datagrams(dgrams: Sequence[bytes]) -> bytes:
+    """Frame datagrams as udp_read_cb does (sr-main.c:163-173) and concatenate them."""
+    L = lib()
+    cap = sum(min(len(d), SR_MAX_DATAGRAM) + 1 for d in dgrams)
+    out = ctypes.create_string_buffer(max(cap, 1))
+    bufs = [ctypes.create_string_buffer(bytes(d), max(len(d), 1)) for d in dgrams]
+    ptrs = (ctypes.c_void_p * max(len(dgrams), 1))(*[ctypes.addressof(b) for b in bufs])
+    lens = (ctypes.c_size_t * max(len(dgrams), 1))(*[len(d) for d in dgrams])
+    n = L.sr_frame_datagrams(out, cap, ptrs, lens, len(dgrams))
+    if n == ctypes.c_size_t(-1).value:
+        raise SrError(errno.ENOSPC, "sr_frame_datagrams")
+    return out.raw[:n]
+
+
+# ---- synthetic traffic ------------------------------------------------------------------------
+GEN_FIXED, GEN_TEST_SHAPE = 0, 1
+
+
+@dataclass
+class Stream:
+    data: np.ndarray          # uint8, concatenated framed datagrams
+    dgram_lens: np.ndarray    # uint32
+    n_lines: int
+
+
+def gen_stream(nbytes: int, line_lens: Iterable[int], seed: int, p_invalid: float = 0.0,
+               kind: int = GEN_FIXED, max_dgram: int = SR_MAX_DATAGRAM) -> Stream:
+    """Seeded synthetic stream (statsd-router_amd/csrc/sr_gen.c) of at most nbytes bytes."""
+    g = gen_lib()
+    lens = np.ascontiguousarray(np.array(list(line_lens), dtype=np.uint32))
+    out = np.zeros(max(nbytes, 1), dtype=np.uint8)
+    dcap = nbytes // 6 + 2
+    dl = np.zeros(dcap, dtype=np.uint32)
+    nd, nl = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    n = g.sr_gen_stream(seed, kind, lens.ctypes.data, len(lens), float(p_invalid), max_dgram,
+                        out.ctypes.data, nbytes, dl.ctypes.data, dcap, ctypes.byref(nd), ctypes.byref(nl))
+    return Stream(out[:n], dl[: min(nd.value, dcap)].copy(), nl.value)
+
+
+# ---- the router context -------------------------------------------------------------------------
+def alive_words(n_downstreams: int, alive: Iterable[int] | np.ndarray | None) -> np.ndarray:
+    """Bitmap words from a 0/1 sequence (None = all alive)."""
+    nw = max((n_downstreams + 63) // 64, 1)
+    w = np.zeros(nw, dtype=np.uint64)
+    bits = np.ones(n_downstreams, dtype=bool) if alive is None else np.asarray(list(alive), dtype=bool)
+    for k in np.nonzero(bits)[0]:
+        w[k >> 6] |= np.uint64(1) << np.uint64(k & 63)
+    return w
+
+
+class Router:
+    """One sr_ctx: a HIP stream's worth of routing state on one GPU (sr_open .. sr_close)."""
+
+    def __init__(self, n_downstreams: int, max_batch_bytes: int, device: int = 0):
+        self._lib = lib()
+        self.n_downstreams = n_downstreams
+        self.max_batch_bytes = max_batch_bytes
+        self.device = device
+        h = ctypes.c_void_p()
+        _check(self._lib.sr_open(ctypes.byref(h), device, max_batch_bytes, n_downstreams), "sr_open")
+        self._h = h
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        return self._h
+
+    def close(self) -> None:
+        if self._h:
+            self._lib.sr_close(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_alive(self, alive) -> None:
+        """alive: 0/1 per downstream, or a uint64 word array."""
+        a = np.asarray(alive)
+        w = a.astype(np.uint64) if a.dtype == np.uint64 else alive_words(self.n_downstreams, alive)
+        w = np.ascontiguousarray(w)
+        _check(self._lib.sr_set_alive(self._h, w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))), "sr_set_alive")
+
+    def set_stream(self, stream_handle: int | None) -> None:
+        _check(self._lib.sr_set_stream(self._h, ctypes.c_void_p(stream_handle or 0)), "sr_set_stream")
+
+    def route(self, data: bytes | np.ndarray, max_records: int | None = None, want_hashes: bool = False):
+        """sr_route_batch on host memory. Returns (records[n] structured array, hashes or None, n)."""
+        buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else np.ascontiguousarray(data, dtype=np.uint8)
+        nbytes = int(buf.size)
+        cap = nbytes if max_records is None else max_records
+        out = np.zeros(max(cap, 1), dtype=RECORD_DTYPE)
+        hashes = np.zeros(max(cap, 1), dtype=np.uint64) if want_hashes else None
+        n = ctypes.c_size_t(0)
+        rc = self._lib.sr_route_batch(self._h, buf.ctypes.data if nbytes else None, nbytes, out.ctypes.data,
+                                      cap, ctypes.byref(n), hashes.ctypes.data if want_hashes else None)
+        if rc not in (0, -errno.ENOSPC):
+            _check(rc, "sr_route_batch")
+        k = min(n.value, cap)
+        return out[:k], (hashes[:k] if want_hashes else None), n.value
+
+    def route_device(self, d_bytes: int, nbytes: int, d_out: int, max_records: int,
+                     d_hashes: int | None, d_count: int) -> None:
+        """sr_route_device with raw device pointers (e.g. torch tensors' data_ptr())."""
+        _check(self._lib.sr_route_device(self._h, ctypes.c_void_p(d_bytes), nbytes, ctypes.c_void_p(d_out),
+                                         max_records, ctypes.c_void_p(d_hashes or 0), ctypes.c_void_p(d_count)),
+               "sr_route_device")
+
+    def sync(self) -> None:
+        _check(self._lib.sr_sync(self._h), "sr_sync")
+
+
+def version() -> str:
+    return lib().sr_version().decode()

@@ -1,0 +1,56 @@
+"""Shared fixtures. `-m "not gpu"` runs on the CPU build container; `-m gpu` on an MI355X."""
+from __future__ import annotations
+
+import glob
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through the C ABI)")
+
+
+@pytest.fixture(scope="session")
+def pkg():
+    return importlib.import_module("statsd-router_amd")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import sr_oracle
+
+    return sr_oracle
+
+
+def golden_cases():
+    return sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "*.npz")))
+
+
+def load_case(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))  # allow_pickle=False (default)
+    raw = z["dgram_bytes"].tobytes()
+    lens = z["dgram_lens"].astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)]).tolist()
+    dgrams = [raw[offs[i]:offs[i + 1]] for i in range(len(lens))]
+    return {
+        "dgrams": dgrams,
+        "alive": z["alive"],
+        "n": int(z["n_downstreams"][0]),
+        "records": z["records"],
+        "hashes": z["hashes"],
+    }
+
+
+def load_digests():
+    with open(os.path.join(GOLDEN, "digests.json")) as f:
+        return json.load(f)
