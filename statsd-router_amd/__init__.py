@@ -70,6 +70,14 @@ def verdicts(routes: np.ndarray) -> np.ndarray:
 
 
 def _load_route_lib() -> ctypes.CDLL:
+    # One HIP runtime per process: PyTorch-ROCm wheels bundle their own libamdhip64.so.7 /
+    # libhsa-runtime64.so.1 (same sonames as /opt/rocm's). If torch is importable, load it first
+    # so libsr_route.so binds to the runtime torch already uses (a second HSA runtime in the same
+    # process cannot open the GPUs).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(ROUTE_LIB):
         raise ImportError(
             f"{ROUTE_LIB} is missing: build it with __graft_entry__.build() or `make -C statsd-router_amd`"

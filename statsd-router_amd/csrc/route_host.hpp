@@ -1,0 +1,189 @@
+// route_host.hpp — host-side helpers shared by the C ABI (sr_route.hip) and the ablation tool:
+// divisor reciprocals, power tables, per-context device state and the launch sequence.
+#pragma once
+
+#include <errno.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <vector>
+
+#include "route_kernel.hpp"
+
+namespace srk {
+
+inline Magic make_magic(uint64_t d) {
+    Magic mg{0, 0, 0};
+    if (d == 0) return mg;
+    const int fl = 63 - __builtin_clzll(d);
+    if ((d & (d - 1)) == 0) {
+        mg.shift = (uint32_t)fl;
+        return mg;
+    }
+    const unsigned __int128 num = (unsigned __int128)1 << (64 + fl);
+    uint64_t pm = (uint64_t)(num / d);
+    const uint64_t rem = (uint64_t)(num % d);
+    const uint64_t e = d - rem;
+    if (e < (1ull << fl)) {
+        mg.kind = 1;
+    } else {
+        pm += pm;
+        const uint64_t twice = rem + rem;
+        if (twice >= d || twice < rem) pm += 1;
+        mg.kind = 2;
+    }
+    mg.m = pm + 1;
+    mg.shift = (uint32_t)fl;
+    return mg;
+}
+
+inline uint64_t host_div(uint64_t n, const Magic &mg) {
+    if (mg.kind == 0) return n >> mg.shift;
+    const uint64_t t = (uint64_t)(((unsigned __int128)mg.m * n) >> 64);
+    if (mg.kind == 1) return t >> mg.shift;
+    return (((n - t) >> 1) + t) >> mg.shift;
+}
+
+// Device state owned by one context (one stream at a time).
+struct DeviceState {
+    uint32_t nds = 0, nwords = 0, dead = 0, max_tiles = 0, pending_cap = 0;
+    size_t max_batch = 0;
+    Magic magic_n{0, 0, 0};
+    uint64_t *h_alive = nullptr;
+    uint64_t *d_alive = nullptr;
+    Magic *d_magic = nullptr;
+    uint64_t *d_kpow = nullptr;
+    Control *d_ctl = nullptr;
+    uint64_t *d_status = nullptr;
+    PendingLine *d_pending = nullptr;
+
+    int init(size_t max_batch_bytes, uint32_t n_downstreams) {
+        max_batch = max_batch_bytes;
+        nds = n_downstreams;
+        nwords = (n_downstreams + 63) / 64;
+        max_tiles = (uint32_t)((max_batch_bytes + 16383) / 16384);   // enough for the smallest tile (256 threads)
+        h_alive = (uint64_t *)calloc(nwords ? nwords : 1, sizeof(uint64_t));
+        if (!h_alive) return -ENOMEM;
+        if (hipMalloc(&d_alive, (nwords ? nwords : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+        if (hipMalloc(&d_magic, (n_downstreams + 1) * sizeof(Magic)) != hipSuccess) return -ENOMEM;
+        if (hipMalloc(&d_kpow, kPowTable * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+        if (hipMalloc(&d_ctl, sizeof(Control)) != hipSuccess) return -ENOMEM;
+        if (hipMalloc(&d_status, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+        if (hipMemset(d_ctl, 0, sizeof(Control)) != hipSuccess) return -EIO;
+        if (hipMemset(d_status, 0, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -EIO;
+        std::vector<Magic> mg(n_downstreams + 1);
+        for (uint32_t d = 1; d <= n_downstreams; ++d) {
+            mg[d] = make_magic(d);
+            // self-check of the reciprocal against the hardware divide on awkward numerators
+            const uint64_t probes[6] = {0ull, 1ull, d - 1ull, (uint64_t)d, ~0ull, 0x9E3779B97F4A7C15ull * d + 7};
+            for (uint64_t nn : probes)
+                if (host_div(nn, mg[d]) != nn / d) return -EIO;
+        }
+        magic_n = n_downstreams ? mg[n_downstreams] : Magic{0, 0, 0};
+        if (hipMemcpy(d_magic, mg.data(), mg.size() * sizeof(Magic), hipMemcpyHostToDevice) != hipSuccess)
+            return -EIO;
+        std::vector<uint64_t> kp(kPowTable);
+        for (int i = 0; i < 64; ++i) {
+            kp[i] = ipow(K, (unsigned)i);
+            kp[64 + i] = ipow(K, 64u * (unsigned)i);
+            kp[128 + i] = ipow(kKinv, (unsigned)i);
+        }
+        if (hipMemcpy(d_kpow, kp.data(), kp.size() * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess)
+            return -EIO;
+        for (uint32_t i = 0; i < n_downstreams; ++i) h_alive[i >> 6] |= 1ull << (i & 63);
+        if (hipMemcpy(d_alive, h_alive, (nwords ? nwords : 1) * sizeof(uint64_t), hipMemcpyHostToDevice) !=
+            hipSuccess)
+            return -EIO;
+        dead = 0;
+        return 0;
+    }
+
+    void release() {
+        (void)hipFree(d_alive);
+        (void)hipFree(d_magic);
+        (void)hipFree(d_kpow);
+        (void)hipFree(d_ctl);
+        (void)hipFree(d_status);
+        (void)hipFree(d_pending);
+        free(h_alive);
+        d_alive = nullptr;
+        d_magic = nullptr;
+        d_kpow = nullptr;
+        d_ctl = nullptr;
+        d_status = nullptr;
+        d_pending = nullptr;
+        h_alive = nullptr;
+    }
+
+    int set_alive(const uint64_t *alive, hipStream_t stream) {
+        uint32_t live = 0;
+        for (uint32_t w = 0; w < nwords; ++w) {
+            uint64_t v = alive[w];
+            if (w == nwords - 1 && (nds & 63)) v &= (1ull << (nds & 63)) - 1;
+            h_alive[w] = v;
+            live += (uint32_t)__builtin_popcountll(v);
+        }
+        dead = nds - live;
+        if (nwords && hipMemcpyAsync(d_alive, h_alive, nwords * sizeof(uint64_t), hipMemcpyHostToDevice, stream) !=
+                          hipSuccess)
+            return -EIO;
+        if (dead > (uint32_t)kOverlay && !d_pending) {
+            pending_cap = (uint32_t)(max_batch / SR_MIN_LINE_LENGTH + 1);
+            if (hipMalloc(&d_pending, (size_t)pending_cap * sizeof(PendingLine)) != hipSuccess) {
+                d_pending = nullptr;
+                pending_cap = 0;
+                return -ENOMEM;
+            }
+        }
+        // the copy reads h_alive: complete it before the snapshot can change again
+        return hipStreamSynchronize(stream) == hipSuccess ? 0 : -EIO;
+    }
+
+    RouteParams params(const uint8_t *d_bytes, size_t nbytes, sr_record *d_out, size_t max_records,
+                       uint64_t *d_hashes, uint64_t *d_n) const {
+        RouteParams p;
+        p.bytes = d_bytes;
+        p.nbytes = (uint32_t)nbytes;
+        p.ntiles = (uint32_t)(((uint64_t)nbytes + kTile - 1) / kTile);
+        p.recs = d_out;
+        p.hashes = d_hashes;
+        p.n_out = d_n;
+        p.max_records = (uint32_t)(max_records > 0xFFFFFFFFull ? 0xFFFFFFFFull : max_records);
+        p.nds = nds;
+        p.dead = dead;
+        p.pending_cap = pending_cap;
+        p.magic_n = magic_n;
+        p.alive = d_alive;
+        p.magic = d_magic;
+        p.kpow = d_kpow;
+        p.ctl = d_ctl;
+        p.status = d_status;
+        p.pending = d_pending;
+        return p;
+    }
+
+    bool wide() const { return dead > (uint32_t)kOverlay && dead < nds; }
+};
+
+template <int BLOCK, unsigned ABL>
+inline int launch_route(const DeviceState &ds, RouteParams p, hipStream_t stream) {
+    constexpr uint32_t T = BLOCK * kLaneBytes;
+    p.ntiles = (uint32_t)(((uint64_t)p.nbytes + T - 1) / T);
+    if (ds.wide() && hipMemsetAsync(&ds.d_ctl->pending, 0, sizeof(uint32_t), stream) != hipSuccess) return -EIO;
+    hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.ntiles), dim3(BLOCK), 0, stream, p);
+    if (hipGetLastError() != hipSuccess) return -EIO;
+    if (ds.wide()) {
+        static bool attr_set = false;
+        if (!attr_set) {
+            (void)hipFuncSetAttribute((const void *)probe_wide_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024);
+            attr_set = true;
+        }
+        hipLaunchKernelGGL(probe_wide_kernel, dim3(256), dim3(64), (size_t)ds.nds * sizeof(uint16_t), stream, p);
+        if (hipGetLastError() != hipSuccess) return -EIO;
+    }
+    return 0;
+}
+
+}  // namespace srk

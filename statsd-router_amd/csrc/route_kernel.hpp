@@ -1,0 +1,783 @@
+// route_kernel.hpp — device side of the MI355X statsd-router hot path (included by sr_route.hip
+// and by tools/ablate_route.hip; everything lives in namespace srk).
+//
+// Reference path (hulu/statsd-router, /root/reference):
+//   udp_read_cb        sr-main.c:149-191  framing + newline tokeniser + length gate 5 < L < 1450
+//   process_data_line  sr-main.c:137-147  ':' presence -> INVALID_FORMAT
+//   hash               sr-main.c:120-134  sdbm over the name (signed char, u64 wrap)
+//   find_downstream    sr-main.c:86-117   hash-seeded partial Fisher-Yates probe over alive shards
+//
+// Input: a batch of framed datagrams back to back in HBM. Every framed datagram ends in '\n'
+// (host framing, sr_frame_datagram), so the lines of the batch are its '\n'-terminated pieces and
+// datagram boundaries are irrelevant here. Output: one 8-byte sr_record per line, in input order.
+//
+// One kernel, one pass over the bytes:
+//   * 64 KiB tiles, tile = blockIdx.x, one 1024-thread workgroup each (one per CU).
+//   * Tile bytes: coalesced 1 KiB-per-wave-instruction buffer loads -> LDS; each lane then owns
+//     64 contiguous bytes.
+//   * Per lane: '\n' and ':' bitmasks (SWAR) and the unmasked sdbm Horner value of its 64 bytes.
+//     The name hash of a line [s, c) is a difference of Horner prefixes,
+//         h = P(c-1) - P(s-1) * K^(c-s)   (mod 2^64, K = 65599),
+//     P over the tile comes from a wave + workgroup scan of the lane values (multiplier K^64) and
+//     is stored per 16-byte piece in LDS.
+//   * Line numbering: a workgroup scan of per-lane '\n' counts gives tile-local line indices; the
+//     tile's first record index comes from a decoupled look-back over per-tile counts (8-byte
+//     {epoch, flag, count} granules written and polled with agent-scope relaxed atomics: the data
+//     is the flag). A tile publishes its count straight after its loads; one wave polls up to
+//     1024 predecessors per round while the other waves stage their lines. A predecessor that has
+//     not published within a bounded spin is counted by the waiting wave itself, so progress
+//     never depends on dispatch order.
+//   * The line that straddles into the tile (at most one) is finished by the last wave from the
+//     1 KiB before the tile, loaded at kernel start (further windows only for lines > 1 KiB).
+//   * Shard pick: h % N through a 64-bit magic reciprocal when every shard is alive; otherwise
+//     the reference's probe with a 16-entry register overlay of the permutation (each dead shard
+//     is probed at most once per line). Lines needing more than 16 dead probes are deferred to
+//     probe_wide_kernel (the probe on a full LDS permutation).
+//   * The last workgroup out (8-way sharded arrival counters) advances the context's epoch, so
+//     stale look-back granules of earlier launches are never mistaken for current ones, with or
+//     without graph replay.
+// No MFMA: HBM-bound byte work on VALU + LDS.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sr_route.h"
+
+namespace srk {
+
+constexpr int kBlock = 1024;                 // threads per workgroup of the product kernel (16 waves)
+constexpr int kLaneBytes = 64;               // bytes per lane
+constexpr int kTile = kBlock * kLaneBytes;   // 64 KiB per tile
+constexpr int kOverlay = 16;                 // register overlay entries of the probe
+constexpr int kNone = 0x1FFFF;               // "no colon" marker (above any tile position)
+constexpr int kSpinBudget = 1 << 14;         // polls before a missing predecessor is proxied
+constexpr uint32_t kFlagAgg = 1u, kFlagIncl = 2u;
+constexpr uint16_t kRoutePending = 0xFFFCu;  // internal: resolved by probe_wide_kernel
+constexpr uint64_t K = 65599ull;             // sdbm multiplier: (h<<6)+(h<<16)-h (sr-main.c:131)
+constexpr int kPowTable = 192;               // K^i, K^(64 i), K^-i for i < 64 (copied to LDS per tile)
+
+// ablation switches (tools/ablate_route.hip); the product instantiates ABL_NONE
+enum : unsigned {
+    ABL_NONE = 0,
+    ABL_NO_LOOKBACK = 1u,   // base = 0 (records overwrite each other)
+    ABL_NO_LINES = 2u,      // skip per-line staging / hashing / records
+    ABL_NO_PROLOGUE = 4u,   // skip the straddling-line prologue
+    ABL_NO_SCAN = 8u,       // skip masks/Horner/scans (counts only)
+    ABL_LOAD_ONLY = 16u,    // load the tile into LDS and count '\n' only
+};
+
+constexpr uint64_t ipow(uint64_t b, unsigned e) {
+    uint64_t r = 1;
+    while (e) {
+        if (e & 1) r *= b;
+        b *= b;
+        e >>= 1;
+    }
+    return r;
+}
+constexpr uint64_t inv_odd(uint64_t a) {  // a^-1 mod 2^64 for odd a (Newton)
+    uint64_t x = a;
+    for (int i = 0; i < 6; ++i) x *= 2 - a * x;
+    return x;
+}
+constexpr uint64_t kK16 = ipow(K, 16), kK32 = ipow(K, 32), kK48 = ipow(K, 48), kK64 = ipow(K, 64);
+constexpr uint64_t kK4096 = ipow(K, 4096);
+constexpr uint64_t kK4 = ipow(K, 4);
+constexpr int32_t kK2lo = (int32_t)(K * K - (1ull << 32));   // K^2 = 2^32 + 0x7E0F81
+static_assert(K * K == (1ull << 32) + 0x7E0F81ull, "K^2 split");
+constexpr uint64_t kKinv = inv_odd(K);
+static_assert(K * kKinv == 1ull, "K inverse");
+
+struct Magic {          // exact n / d for 64-bit n (Granlund-Montgomery, round-up variant)
+    uint64_t m;
+    uint32_t shift;
+    uint32_t kind;      // 0: q = n >> shift; 1: q = mulhi >> shift; 2: add-indicator form
+};
+
+struct PendingLine {
+    uint32_t rec;
+    uint32_t pad;
+    uint64_t hash;
+};
+
+// Per-context device control block, zeroed once at sr_open. Counters on separate 128-B lines.
+struct Control {
+    uint32_t epoch;
+    uint32_t top;
+    uint32_t pending;
+    uint32_t pad0[29];
+    uint32_t done[8][32];
+};
+
+struct RouteParams {
+    const uint8_t *bytes;
+    uint32_t nbytes;
+    uint32_t ntiles;
+    sr_record *recs;
+    uint64_t *hashes;        // may be null
+    uint64_t *n_out;         // device: total line count
+    uint32_t max_records;
+    uint32_t nds;            // number of downstreams
+    uint32_t dead;           // dead downstreams in the alive snapshot
+    uint32_t pending_cap;
+    Magic magic_n;           // for h % nds (fast path)
+    const uint64_t *alive;   // bitmap
+    const Magic *magic;      // [0..nds], index i -> divisor i
+    const uint64_t *kpow;    // kPowTable entries: K^i, K^(64 i), K^-i (i < 64)
+    Control *ctl;
+    uint64_t *status;        // per-tile look-back granules
+    PendingLine *pending;
+};
+
+// ---------------------------------------------------------------------------------------
+// Helpers
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t sdbm_step(uint64_t h, uint32_t byte) {
+    // sr-main.c:131: h = (h << 6) + (h << 16) - h + c, with c a *signed* char (sr-main.c:122)
+    const int64_t c = (int8_t)byte;
+    return (h << 16) + (h << 6) - h + (uint64_t)c;
+}
+
+// Four Horner steps at once (bytes in memory order = little-endian byte order of x):
+//   h*K^4 + (c0*K + c1)*K^2 + (c2*K + c3),   K^2 = 2^32 + 0x7E0F81.
+// The pair terms are exact 32-bit multiply-adds; only the final step needs 64-bit multiplies,
+// so the dword costs one 64x64 product instead of four (the 64-bit multiplies are the slow ops).
+__device__ __forceinline__ uint64_t sdbm_dword(uint64_t h, uint32_t x) {
+    const int32_t c0 = (int8_t)(x & 0xFFu), c1 = (int8_t)((x >> 8) & 0xFFu);
+    const int32_t c2 = (int8_t)((x >> 16) & 0xFFu), c3 = (int8_t)(x >> 24);
+    const int32_t t = c0 * (int32_t)K + c1;
+    const int32_t u = c2 * (int32_t)K + c3;
+    const uint64_t d = (uint64_t)((int64_t)t * kK2lo) + (uint64_t)(int64_t)u + ((uint64_t)(uint32_t)t << 32);
+    return h * kK4 + d;
+}
+
+// keep the bytes of dword x whose index within it is >= lo and < hi (0..4)
+__device__ __forceinline__ uint32_t byte_range(uint32_t x, int lo, int hi) {
+    const uint32_t mlo = lo <= 0 ? 0xFFFFFFFFu : (lo >= 4 ? 0u : ~((1u << (8 * lo)) - 1u));
+    const uint32_t mhi = hi >= 4 ? 0xFFFFFFFFu : (hi <= 0 ? 0u : ((1u << (8 * hi)) - 1u));
+    return x & mlo & mhi;
+}
+
+// Horner of the bytes of a 16-byte piece whose piece index is in [lo, hi), others zeroed.
+__device__ __forceinline__ uint64_t sdbm_piece(uint4 v, int lo, int hi) {
+    uint64_t h = 0;
+    h = sdbm_dword(h, byte_range(v.x, lo, hi));
+    h = sdbm_dword(h, byte_range(v.y, lo - 4, hi - 4));
+    h = sdbm_dword(h, byte_range(v.z, lo - 8, hi - 8));
+    return sdbm_dword(h, byte_range(v.w, lo - 12, hi - 12));
+}
+
+// 4-bit mask of the bytes of x equal to the byte replicated in pat (exact SWAR test).
+__device__ __forceinline__ uint32_t eq_mask4(uint32_t x, uint32_t pat) {
+    const uint32_t t = x ^ pat;
+    const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+    return (((z >> 7) * 0x00204081u) >> 21) & 0xFu;
+}
+
+__device__ __forceinline__ uint32_t eq_mask16(uint4 v, uint32_t pat) {
+    return eq_mask4(v.x, pat) | (eq_mask4(v.y, pat) << 4) | (eq_mask4(v.z, pat) << 8) |
+           (eq_mask4(v.w, pat) << 12);
+}
+
+// number of bytes equal to the replicated pattern
+__device__ __forceinline__ uint32_t eq_count4(uint32_t x, uint32_t pat) {
+    const uint32_t t = x ^ pat;
+    const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+    return __popc(z);
+}
+
+typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint4 as_uint4(v4u32 r) { return make_uint4(r[0], r[1], r[2], r[3]); }
+
+// 16 bytes at `off`; bytes at or past `n` read as 0. Only the one piece that straddles the end
+// of the batch takes the byte-wise path (buffer range checks are not byte-exact for dwordx4).
+__device__ __forceinline__ uint4 load16(__amdgpu_buffer_rsrc_t rsrc, uint32_t off, uint32_t n) {
+    if (off + 16u <= n) return as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0));
+    uint64_t lo = 0, hi = 0;
+    for (uint32_t i = 0; i < 16u && off + i < n; ++i) {
+        const uint64_t b = __builtin_amdgcn_raw_buffer_load_b8(rsrc, off + i, 0, 0);
+        if (i < 8) lo |= b << (8 * i);
+        else hi |= b << (8 * (i - 8));
+    }
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
+
+__device__ __forceinline__ uint64_t div_magic(uint64_t n, const Magic &mg) {
+    if (mg.kind == 0) return n >> mg.shift;
+    const uint64_t t = __umul64hi(mg.m, n);
+    if (mg.kind == 1) return t >> mg.shift;
+    return (((n - t) >> 1) + t) >> mg.shift;
+}
+
+__device__ __forceinline__ uint32_t mod_magic(uint64_t n, const Magic &mg, uint32_t d) {
+    return (uint32_t)(n - div_magic(n, mg) * (uint64_t)d);
+}
+
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v, int d) {
+    const uint32_t lo = __shfl_up((uint32_t)v, d, 64);
+    const uint32_t hi = __shfl_up((uint32_t)(v >> 32), d, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int d) {
+    const uint32_t lo = __shfl_xor((uint32_t)v, d, 64);
+    const uint32_t hi = __shfl_xor((uint32_t)(v >> 32), d, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += shfl_xor64(v, d);
+    return v;
+}
+
+__device__ __forceinline__ int wave_max_i32(int v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v = max(v, __shfl_xor(v, d, 64));
+    return v;
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Segmented "line state" scan element: [63:32] newline count, [31] lane range holds a '\n',
+// [16:0] first ':' of the line open at the right end of the range (tile position, kNone = none).
+// combine(f, g) for f left of g: counts add; if g holds a '\n' its state wins, else the open
+// line continues from f and its first colon is the earlier one.
+__device__ __forceinline__ uint64_t seg_combine(uint64_t f, uint64_t g) {
+    const uint64_t cnt = (f & 0xFFFFFFFF00000000ull) + (g & 0xFFFFFFFF00000000ull);
+    uint32_t lo;
+    if ((uint32_t)g & 0x80000000u) {
+        lo = (uint32_t)g;
+    } else {
+        const uint32_t fc = (uint32_t)f & 0x1FFFFu, gc = (uint32_t)g & 0x1FFFFu;
+        lo = ((uint32_t)f & 0x80000000u) | (fc < gc ? fc : gc);
+    }
+    return cnt | lo;
+}
+
+__device__ __forceinline__ uint64_t mk_status(uint32_t epoch, uint32_t flag, uint32_t value) {
+    return ((uint64_t)(epoch & 0x3FFFFFFFu) << 34) | ((uint64_t)flag << 32) | value;
+}
+
+__device__ __forceinline__ bool alive_bit(const uint64_t *alive, uint32_t k) {
+    return (alive[k >> 6] >> (k & 63)) & 1ull;
+}
+
+// find_downstream (sr-main.c:86-117) for one line. Returns the shard, SR_ROUTE_ALL_DEAD, or
+// kRoutePending if more than kOverlay dead shards had to be probed.
+__device__ uint32_t probe_shard(uint64_t h, const RouteParams &p) {
+    const uint32_t n = p.nds;
+    if (p.dead >= n) return SR_ROUTE_ALL_DEAD;            // includes N == 0
+    if (p.dead == 0) return mod_magic(h, p.magic_n, n);   // every shard alive: j = h % N
+    // ds_index[] is the identity plus an overlay of (position -> value) writes, newest last.
+    uint32_t ov[kOverlay];   // (pos << 16) | value
+    int nov = 0;
+#pragma unroll
+    for (int e = 0; e < kOverlay; ++e) ov[e] = 0xFFFFFFFFu;
+    for (uint32_t i = n; i > 0; --i) {
+        const Magic mg = p.magic[i];
+        const uint32_t j = mod_magic(h, mg, i);                      // :98
+        uint32_t k = j;                                              // :99
+#pragma unroll
+        for (int e = 0; e < kOverlay; ++e)
+            if ((ov[e] >> 16) == j) k = ov[e] & 0xFFFFu;
+        if (alive_bit(p.alive, k)) return k;                         // :101-104
+        if (j != i - 1) {                                            // :108-111
+            uint32_t v = i - 1;
+#pragma unroll
+            for (int e = 0; e < kOverlay; ++e)
+                if ((ov[e] >> 16) == i - 1) v = ov[e] & 0xFFFFu;
+            if (nov == kOverlay) return kRoutePending;
+#pragma unroll
+            for (int e = 0; e < kOverlay; ++e)
+                if (e == nov) ov[e] = (j << 16) | v;
+            ++nov;
+        }
+        h = (h * 7 + 5) / 3;                                         // :113
+    }
+    return SR_ROUTE_ALL_DEAD;                                        // :115-116
+}
+
+// ---------------------------------------------------------------------------------------
+// The route kernel
+// ---------------------------------------------------------------------------------------
+template <int BLOCK>
+struct SmemT {
+    static constexpr int kWaves = BLOCK / 64;
+    static constexpr int kTileB = BLOCK * kLaneBytes;
+    static constexpr int kPiecesB = kTileB / 16;
+    static constexpr int kWin = BLOCK >= 512 ? 2048 : 1024;   // tile-local lines staged per round
+    uint4 tile[kPiecesB];            // the tile's bytes
+    uint64_t pstate[kPiecesB];       // P(16p - 1) for every 16-byte piece p (tile frame, P(-1)=0)
+    uint32_t lend[kWin + 1];         // per staged line: position of its '\n'; slot 0 = previous line
+    int32_t lcol[kWin + 1];          // per staged line: first ':' (kNone if none; < 0: before the tile)
+    uint64_t wave_seg[kWaves];
+    uint64_t wave_hash[kWaves];
+    uint32_t wave_cnt[kWaves];
+    uint64_t kp_lo[64];              // K^i
+    uint64_t kp_hi[64];              // K^(64 i)
+    uint64_t kinv[64];               // K^-i
+    uint64_t h_pre, hc_pre;          // straddling line: Horner of [s_pre, 0) and [s_pre, c_pre)
+    int32_t s_pre, c_pre;            // tile-relative start / first colon (c_pre: kNone if none)
+    uint32_t epoch, base;
+};
+
+// K^n for 0 <= n < 4096 from the LDS tables
+template <class S>
+__device__ __forceinline__ uint64_t kpow_n(const S &sm, int n) {
+    return sm.kp_hi[n >> 6] * sm.kp_lo[n & 63];
+}
+
+// P(x) in the tile frame for -1 <= x < tile: Horner of tile bytes [0, x].
+template <class S>
+__device__ __forceinline__ uint64_t prefix_at(const S &sm, int x) {
+    if (x < 0) return 0;
+    const int pc = x >> 4, r = x & 15;
+    const uint64_t t = sdbm_piece(sm.tile[pc], 0, r + 1);
+    // t = Horner(bytes[16pc .. x]) * K^(15 - r); undo the trailing zeros with K^-1.
+    return sm.pstate[pc] * sm.kp_lo[r + 1] + t * sm.kinv[15 - r];
+}
+
+// Number of '\n' bytes in tile m, counted by one wave (only used when a predecessor has not
+// published its count within the spin budget).
+template <int BLOCK>
+__device__ uint32_t count_tile_wave(const RouteParams &p, __amdgpu_buffer_rsrc_t rsrc, uint32_t m, int lane) {
+    constexpr uint32_t T = BLOCK * kLaneBytes;
+    uint32_t c = 0;
+    for (uint32_t off = lane * 16; off < T; off += 1024) {
+        const uint4 v = load16(rsrc, m * T + off, p.nbytes);
+        c += eq_count4(v.x, 0x0A0A0A0Au) + eq_count4(v.y, 0x0A0A0A0Au) + eq_count4(v.z, 0x0A0A0A0Au) +
+             eq_count4(v.w, 0x0A0A0A0Au);
+    }
+    return (uint32_t)wave_sum64(c);
+}
+
+// Exclusive line prefix of tile t: decoupled look-back by ONE wave,
+// 256 predecessors per round, stopping at the nearest inclusive prefix. Every lane returns the same value.
+template <int BLOCK>
+__device__ uint32_t look_back_wave(const RouteParams &p, __amdgpu_buffer_rsrc_t rsrc, uint32_t t, uint32_t epoch,
+                                   int lane) {
+    constexpr int kPer = 4;
+    uint64_t acc = 0;
+    int64_t hi = t;
+    const uint32_t ep = epoch & 0x3FFFFFFFu;
+    while (hi > 0) {
+        const int64_t lo = hi - 64 * kPer > 0 ? hi - 64 * kPer : 0;
+        uint64_t st[kPer];
+        bool need[kPer];
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            need[k] = hi - 1 - lane - 64 * k >= lo;
+            st[k] = 0;
+        }
+        for (int spin = 0;; ++spin) {
+            bool pending = false;
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) {
+                if (!need[k]) continue;
+                st[k] = __hip_atomic_load(&p.status[hi - 1 - lane - 64 * k], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+                need[k] = !((uint32_t)(st[k] >> 34) == ep && ((st[k] >> 32) & 3u) != 0);
+                pending |= need[k];
+            }
+            if (!__ballot(pending)) break;
+            if (spin >= kSpinBudget) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        // predecessors still silent: count their tiles here (never needed under in-order
+        // dispatch; it makes progress independent of dispatch order)
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            uint64_t mask = __ballot(need[k]);
+            while (mask) {
+                const int L = __builtin_ctzll(mask);
+                mask &= mask - 1;
+                const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(hi - 1 - L - 64 * k), L);
+                const uint32_t cnt = count_tile_wave<BLOCK>(p, rsrc, m, lane);
+                if (lane == L) {
+                    st[k] = mk_status(epoch, kFlagAgg, cnt);
+                    need[k] = false;
+                }
+            }
+        }
+        int near = -1;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int64_t idx = hi - 1 - lane - 64 * k;
+            if (idx >= lo && ((st[k] >> 32) & 3u) == kFlagIncl) near = max(near, (int)idx);
+        }
+        near = wave_max_i32(near);
+        uint64_t part = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int64_t idx = hi - 1 - lane - 64 * k;
+            if (idx >= lo && idx >= near) part += st[k] & 0xFFFFFFFFull;
+        }
+        acc += wave_sum64(part);
+        if (near >= 0) break;
+        hi = lo;
+    }
+    return (uint32_t)acc;
+}
+
+template <int BLOCK, unsigned ABL>
+__global__ __launch_bounds__(BLOCK, 4) void route_kernel(RouteParams p) {
+    using S = SmemT<BLOCK>;
+    constexpr int kWaves = S::kWaves;
+    constexpr int kTileB = S::kTileB;
+    constexpr int kWin = S::kWin;
+    constexpr int kPreWave = kWaves - 1;   // the wave that finishes the straddling line
+    __shared__ S sm;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const uint32_t t = blockIdx.x;
+    const int64_t T0 = (int64_t)t * kTileB;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)p.bytes, (short)0, (int)p.nbytes, 0x00020000);
+
+    if (tid == 0) sm.epoch = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < kPowTable) (&sm.kp_lo[0])[tid] = p.kpow[tid];   // kp_lo | kp_hi | kinv are contiguous
+    // the 1 KiB before the tile (straddling line), issued together with the tile loads
+    uint4 pre0 = make_uint4(0, 0, 0, 0);
+    if (!(ABL & ABL_NO_PROLOGUE) && wave == kPreWave && t > 0)
+        pre0 = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)(T0 - 1024) + lane * 16, 0, 0));
+    // coalesced tile load: wave instruction k of thread tid covers bytes k*BLOCK*16 + tid*16;
+    // the '\n' count is taken from the registers so the tile's aggregate can be published early
+    {
+        uint4 v[4];
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = load16(rsrc, (uint32_t)T0 + k * BLOCK * 16 + tid * 16, p.nbytes);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            sm.tile[k * BLOCK + tid] = v[k];
+            cnt += eq_count4(v[k].x, 0x0A0A0A0Au) + eq_count4(v[k].y, 0x0A0A0A0Au) +
+                   eq_count4(v[k].z, 0x0A0A0A0Au) + eq_count4(v[k].w, 0x0A0A0A0Au);
+        }
+        cnt = (uint32_t)wave_sum64(cnt);
+        if (lane == 0) sm.wave_cnt[wave] = cnt;
+    }
+    __syncthreads();
+    const uint32_t epoch = sm.epoch;
+    uint32_t tile_count = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) tile_count += sm.wave_cnt[w];
+    if (tid == 0) {   // publish this tile's aggregate (tile 0: its inclusive prefix)
+        const uint64_t st = mk_status(epoch, t == 0 ? kFlagIncl : kFlagAgg, tile_count);
+        __hip_atomic_store(&p.status[t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+
+    // ---- one wave: the line that straddles into this tile (starts before T0) ------------------
+    if (wave == kPreWave && !(ABL & ABL_NO_PROLOGUE)) {
+        int64_t s_abs = 0;
+        if (t > 0) {
+            uint32_t nl16 = eq_mask16(pre0, 0x0A0A0A0Au);
+            uint64_t m = __ballot(nl16 != 0);
+            int64_t a = T0 - 1024 + lane * 16;
+            if (!m) {   // line longer than 1 KiB: keep searching backwards
+                int64_t hi = T0 - 1024;
+                while (hi > 0 && !m) {
+                    const int64_t lo = hi - 1024 > 0 ? hi - 1024 : 0;
+                    a = lo + lane * 16;
+                    nl16 = 0;
+                    if (a < hi) nl16 = eq_mask16(load16(rsrc, (uint32_t)a, p.nbytes), 0x0A0A0A0Au);
+                    m = __ballot(nl16 != 0);
+                    hi = lo;
+                }
+            }
+            if (m) {
+                const int L = 63 - __builtin_clzll(m);
+                const int64_t last = a + 31 - __builtin_clz(nl16 | 1u);   // valid on lane L
+                s_abs = (int64_t)readlane64((uint64_t)last, L) + 1;
+            }
+        }
+        const int32_t s_pre = (int32_t)(s_abs - T0);
+        uint64_t h_pre = 0, hc_pre = 0;
+        int32_t c_pre = kNone;
+        if (s_pre < 0 && -s_pre <= (int)SR_MAX_LINE_LENGTH - 1) {
+            // windows of 64 pieces: w = 1 is [T0-2048, T0-1024) (only for lines over 1 KiB)
+            const int nwin = -s_pre > 1024 ? 2 : 1;
+            uint4 pw[2];
+            pw[0] = pre0;
+            pw[1] = nwin == 2 ? load16(rsrc, (uint32_t)(T0 - 2048) + lane * 16, p.nbytes) : make_uint4(0, 0, 0, 0);
+            // first colon at or after s_abs, oldest window first
+            int64_t cabs = -1;
+#pragma unroll
+            for (int w = 1; w >= 0; --w) {
+                if (w >= nwin || cabs >= 0) continue;
+                const int64_t pb = T0 - 1024 * (w + 1) + lane * 16;
+                const int skip = (int)max<int64_t>(0, min<int64_t>(16, s_abs - pb));
+                const uint32_t cm = eq_mask16(pw[w], 0x3A3A3A3Au) & (0xFFFFu << skip) & 0xFFFFu;
+                const uint64_t cb = __ballot(cm != 0);
+                if (cb) {
+                    const int lc = __builtin_ctzll(cb);
+                    cabs = (int64_t)readlane64((uint64_t)(pb + __builtin_ctz(cm | 0x10000u)), lc);
+                }
+            }
+            uint64_t hs = 0, hcs = 0;
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                if (w >= nwin) continue;
+                const int64_t pb = T0 - 1024 * (w + 1) + lane * 16, pe = pb + 16;
+                const int skip = (int)max<int64_t>(0, min<int64_t>(16, s_abs - pb));
+                const uint64_t qv = sdbm_piece(pw[w], skip, 16);
+                hs += qv * kpow_n(sm, (int)(T0 - pe));
+                if (cabs >= 0) {
+                    if (pe <= cabs) hcs += qv * kpow_n(sm, (int)(cabs - pe));
+                    else if (pb < cabs) hcs += sdbm_piece(pw[w], skip, (int)(cabs - pb)) * sm.kinv[pe - cabs];
+                }
+            }
+            h_pre = wave_sum64(hs);
+            if (cabs >= 0) {
+                c_pre = (int32_t)(cabs - T0);
+                hc_pre = wave_sum64(hcs);
+            }
+        }
+        if (lane == 0) {
+            sm.s_pre = s_pre;
+            sm.c_pre = c_pre;
+            sm.h_pre = h_pre;
+            sm.hc_pre = hc_pre;
+        }
+    } else if ((ABL & ABL_NO_PROLOGUE) && tid == 0) {
+        sm.s_pre = 0;
+        sm.c_pre = kNone;
+        sm.h_pre = sm.hc_pre = 0;
+    }
+
+    // ---- per lane: 64 contiguous bytes ---------------------------------------------------------
+    const int o = tid * kLaneBytes;   // tile position of the lane's first byte
+    uint64_t nlm = 0, clm = 0;        // bit i: byte o+i is '\n' / ':'
+    uint64_t q = 0, q16 = 0, q32 = 0, q48 = 0;
+    if (ABL & (ABL_LOAD_ONLY | ABL_NO_SCAN)) {
+#pragma unroll
+        for (int pc = 0; pc < 4; ++pc) nlm |= (uint64_t)eq_mask16(sm.tile[tid * 4 + pc], 0x0A0A0A0Au) << (16 * pc);
+    } else {
+#pragma unroll
+        for (int pc = 0; pc < 4; ++pc) {
+            const uint4 v = sm.tile[tid * 4 + pc];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int sh = 16 * pc + 4 * k;
+                nlm |= (uint64_t)eq_mask4(w[k], 0x0A0A0A0Au) << sh;
+                clm |= (uint64_t)eq_mask4(w[k], 0x3A3A3A3Au) << sh;
+                q = sdbm_dword(q, w[k]);
+            }
+            if (pc == 0) q16 = q;
+            if (pc == 1) q32 = q;
+            if (pc == 2) q48 = q;
+        }
+    }
+    const int ncnt = __popcll(nlm);
+    uint64_t seg;
+    if (nlm) {
+        const int lastb = 63 - __clzll(nlm);
+        const uint64_t after = lastb == 63 ? 0ull : (clm & (~0ull << (lastb + 1)));
+        const uint32_t fc = after ? (uint32_t)(o + __builtin_ctzll(after)) : (uint32_t)kNone;
+        seg = ((uint64_t)ncnt << 32) | 0x80000000u | fc;
+    } else {
+        seg = clm ? (uint32_t)(o + __builtin_ctzll(clm)) : (uint32_t)kNone;
+    }
+    // wave inclusive scans: seg (line state) and q (Horner, multiplier K^64 per lane)
+    uint64_t sseg = seg, shash = q;
+    if (!(ABL & ABL_LOAD_ONLY)) {
+        uint64_t mul = kK64;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t a = shfl_up64(sseg, d);
+            const uint64_t b = shfl_up64(shash, d);
+            if (lane >= d) {
+                sseg = seg_combine(a, sseg);
+                shash = b * mul + shash;
+            }
+            mul *= mul;
+        }
+    }
+    if (lane == 63) {
+        sm.wave_seg[wave] = sseg;
+        sm.wave_hash[wave] = shash;
+    }
+    __syncthreads();
+    uint64_t eseg = shfl_up64(sseg, 1);
+    uint64_t ehash = shfl_up64(shash, 1);
+    if (lane == 0) {
+        eseg = (uint64_t)kNone;   // empty range: count 0, no '\n', no colon
+        ehash = 0;
+    }
+    {
+        uint64_t cseg = (uint64_t)kNone, chash = 0;   // carry of the waves before this one
+        for (int w2 = 0; w2 < wave; ++w2) {
+            cseg = seg_combine(cseg, sm.wave_seg[w2]);
+            chash = chash * kK4096 + sm.wave_hash[w2];
+        }
+        eseg = seg_combine(cseg, eseg);
+        ehash = chash * sm.kp_hi[lane] + ehash;
+    }
+    if (!(ABL & ABL_LOAD_ONLY)) {
+        sm.pstate[tid * 4 + 0] = ehash;
+        sm.pstate[tid * 4 + 1] = ehash * kK16 + q16;
+        sm.pstate[tid * 4 + 2] = ehash * kK32 + q32;
+        sm.pstate[tid * 4 + 3] = ehash * kK48 + q48;
+    }
+    const int s_pre = sm.s_pre;
+    const int c_pre = sm.c_pre;
+
+    // ---- wave 0: decoupled look-back (the other waves stage their lines meanwhile) ------------
+    if (wave == 0) {
+        uint32_t base = 0;
+        if (!(ABL & ABL_NO_LOOKBACK)) {
+            base = look_back_wave<BLOCK>(p, rsrc, t, epoch, lane);
+            if (lane == 0 && t > 0) {
+                const uint64_t st = mk_status(epoch, kFlagIncl, base + tile_count);
+                __hip_atomic_store(&p.status[t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        if (lane == 0) {
+            sm.base = base;
+            if (t == p.ntiles - 1) *p.n_out = (uint64_t)base + tile_count;
+        }
+    }
+
+    // ---- per line: windows of kWin tile-local lines ----------------------------------------------
+    if (!(ABL & (ABL_NO_LINES | ABL_LOAD_ONLY))) {
+        const int lane_first = (int)(eseg >> 32);               // tile-local index of lane's 1st line
+        const bool open_has_nl = (uint32_t)eseg & 0x80000000u;  // a '\n' earlier in the tile
+        int open_fc = (int)((uint32_t)eseg & 0x1FFFFu);         // first ':' of the open line
+        if (!open_has_nl && c_pre != kNone) open_fc = c_pre;    // straddling line: colon before T0
+        if (tid == 0) sm.lend[0] = 0;
+        for (int wbase = 0; wbase < (int)tile_count; wbase += kWin) {
+            // (1) stage (e, c) of the lane's lines that fall into this window
+            if (nlm && lane_first + ncnt > wbase && lane_first < wbase + kWin) {
+                uint64_t m = nlm;
+                int idx = lane_first;
+                int prevb = -1;
+                while (m) {
+                    const int b = __builtin_ctzll(m);
+                    m &= m - 1;
+                    int c;
+                    if (prevb < 0 && open_fc != kNone) {
+                        c = open_fc;
+                    } else {
+                        const uint64_t below = b == 0 ? 0ull : (~0ull >> (64 - b));
+                        const uint64_t above = ~0ull << (prevb + 1);
+                        const uint64_t cm = clm & below & above;
+                        c = cm ? o + __builtin_ctzll(cm) : kNone;
+                    }
+                    if (idx >= wbase && idx < wbase + kWin) {
+                        sm.lend[idx - wbase + 1] = (uint32_t)(o + b);
+                        sm.lcol[idx - wbase + 1] = c;
+                    }
+                    ++idx;
+                    prevb = b;
+                }
+            }
+            __syncthreads();
+            const uint32_t base = sm.base;
+            // (2) one thread per line
+            const int nwin = min(kWin, (int)tile_count - wbase);
+            for (int jj = tid; jj < nwin; jj += BLOCK) {
+                const int j = wbase + jj;
+                const int e = (int)sm.lend[jj + 1];
+                const int c = sm.lcol[jj + 1];
+                const int s = (j == 0) ? s_pre : (int)sm.lend[jj] + 1;
+                const int64_t len = (int64_t)e - s + 1;
+                uint32_t route;
+                uint64_t h = 0;
+                if (len < (int)SR_MIN_LINE_LENGTH || len > (int)SR_MAX_LINE_LENGTH) {   // sr-main.c:180
+                    route = SR_ROUTE_INVALID_LENGTH;
+                } else if (c == kNone || c > e) {                                        // sr-main.c:140
+                    route = SR_ROUTE_INVALID_FORMAT;
+                } else {
+                    if (j == 0) {
+                        h = c < 0 ? sm.hc_pre : sm.h_pre * kpow_n(sm, c) + prefix_at(sm, c - 1);
+                    } else {
+                        h = prefix_at(sm, c - 1) - prefix_at(sm, s - 1) * kpow_n(sm, c - s);
+                    }
+                    route = probe_shard(h, p);
+                }
+                const uint32_t rec = base + (uint32_t)j;
+                if (rec < p.max_records) {
+                    if (route == kRoutePending) {
+                        const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
+                        if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, 0u, h};
+                    }
+                    sr_record r;
+                    r.offset = (uint32_t)(T0 + s);
+                    r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
+                    r.route = (uint16_t)route;
+                    p.recs[rec] = r;
+                    if (p.hashes) p.hashes[rec] = h;
+                }
+            }
+            __syncthreads();
+            if (tid == 0) sm.lend[0] = sm.lend[nwin];
+            __syncthreads();
+        }
+    } else {
+        __syncthreads();
+    }
+
+    // ---- the last workgroup out advances the epoch (8-way sharded arrival counters) ----------
+    if (tid == 0) {
+        const uint32_t s = t & 7u;
+        const uint32_t cnt_s = (p.ntiles - s + 7u) / 8u;   // workgroups b < ntiles with b % 8 == s
+        const uint32_t old = atomicAdd(&p.ctl->done[s][0], 1u);
+        if (old == cnt_s - 1) {
+            __hip_atomic_store(&p.ctl->done[s][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t nsh = p.ntiles < 8 ? p.ntiles : 8u;
+            const uint32_t top = atomicAdd(&p.ctl->top, 1u);
+            if (top == nsh - 1) {
+                __hip_atomic_store(&p.ctl->top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&p.ctl->epoch, epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
+
+// Lines whose probe met more than kOverlay dead shards: run find_downstream (sr-main.c:86-117)
+// literally on a permutation array held in LDS (N <= 65533 -> <= 128 KiB), one line at a time
+// per workgroup. After each line the touched entries are restored by replaying the probe.
+__global__ __launch_bounds__(64) void probe_wide_kernel(RouteParams p) {
+    extern __shared__ uint16_t ds_index[];
+    const uint32_t n = p.nds;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) ds_index[i] = (uint16_t)i;
+    __syncthreads();
+    const uint32_t np = min(__hip_atomic_load(&p.ctl->pending, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                            p.pending_cap);
+    if (threadIdx.x != 0) return;
+    for (uint32_t x = blockIdx.x; x < np; x += gridDim.x) {
+        const PendingLine pl = p.pending[x];
+        uint64_t h = pl.hash;
+        uint32_t route = SR_ROUTE_ALL_DEAD, steps = 0;
+        for (uint32_t i = n; i > 0; --i) {
+            const uint32_t j = mod_magic(h, p.magic[i], i);
+            const uint32_t k = ds_index[j];
+            ++steps;
+            if (alive_bit(p.alive, k)) { route = k; break; }
+            if (j != i - 1) {
+                ds_index[j] = ds_index[i - 1];
+                ds_index[i - 1] = (uint16_t)k;
+            }
+            h = (h * 7 + 5) / 3;
+        }
+        p.recs[pl.rec].route = (uint16_t)route;
+        // restore the identity on every touched position
+        h = pl.hash;
+        for (uint32_t i = n; i > 0 && steps > 0; --i, --steps) {
+            const uint32_t j = mod_magic(h, p.magic[i], i);
+            ds_index[j] = (uint16_t)j;
+            ds_index[i - 1] = (uint16_t)(i - 1);
+            h = (h * 7 + 5) / 3;
+        }
+    }
+}
+
+}  // namespace srk

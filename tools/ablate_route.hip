@@ -1,0 +1,180 @@
+// Ablation of route_kernel on the bench workloads (16 MiB batches of L-byte metrics, 4 shards).
+// Every variant is an instantiation of the same kernel template (route_kernel.hpp: BLOCK threads
+// per workgroup, ABL_* parts switched off). Variants are timed in interleaved rounds in ONE
+// process over the same rotating set of 64 distinct batches, launched back to back from a
+// hipGraph, on S concurrent streams (each stream with its own context state). A plain
+// streaming-read kernel gives the achievable read rate for the same batches.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/ablate_route tools/ablate_route.hip
+// Run:   tools/ablate_route [line_len]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#include <string>
+#include <vector>
+
+#include "../statsd-router_amd/csrc/route_host.hpp"
+
+extern "C" {
+#include "../statsd-router_amd/csrc/sr_gen.c"
+}
+
+using namespace srk;
+
+#define CK(x)                                                                         \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                                  \
+        }                                                                             \
+    } while (0)
+
+__global__ __launch_bounds__(256) void read_kernel(const uint8_t *p, uint32_t n, uint32_t *sink) {
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)p, (short)0, (int)n, 0x00020000);
+    const uint32_t T0 = blockIdx.x * 16384;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint4 v = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, T0 + k * 4096 + threadIdx.x * 16, 0, 0));
+        acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
+constexpr int kMaxS = 4;
+struct Ctx {
+    DeviceState ds[kMaxS];
+    std::vector<uint8_t *> batches;
+    std::vector<size_t> sizes;
+    sr_record *d_out[kMaxS];
+    uint64_t *d_n;
+    size_t max_lines;
+    uint32_t *sink;
+    hipStream_t s[kMaxS];
+    hipEvent_t fork, join[kMaxS];
+};
+
+template <int BLOCK, unsigned V>
+float time_variant(Ctx &c, int S, int reps) {
+    const int B = (int)c.batches.size();
+    auto launch = [&](int i) {
+        const int k = i % B, st = i % S;
+        if (V == 0xFFFFu) {
+            hipLaunchKernelGGL(read_kernel, dim3((c.sizes[k] + 16383) / 16384), dim3(256), 0, c.s[st], c.batches[k],
+                               (uint32_t)c.sizes[k], c.sink);
+        } else {
+            const RouteParams p =
+                c.ds[st].params(c.batches[k], c.sizes[k], c.d_out[st], c.max_lines, nullptr, c.d_n + k);
+            launch_route<BLOCK, V>(c.ds[st], p, c.s[st]);
+        }
+    };
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    CK(hipStreamBeginCapture(c.s[0], hipStreamCaptureModeGlobal));
+    CK(hipEventRecord(c.fork, c.s[0]));
+    for (int st = 1; st < S; ++st) CK(hipStreamWaitEvent(c.s[st], c.fork, 0));
+    for (int i = 0; i < B; ++i) launch(i);
+    for (int st = 1; st < S; ++st) {
+        CK(hipEventRecord(c.join[st], c.s[st]));
+        CK(hipStreamWaitEvent(c.s[0], c.join[st], 0));
+    }
+    CK(hipStreamEndCapture(c.s[0], &g));
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    CK(hipGraphLaunch(ge, c.s[0]));
+    CK(hipStreamSynchronize(c.s[0]));
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventRecord(a, c.s[0]));
+    for (int r = 0; r < reps; ++r) CK(hipGraphLaunch(ge, c.s[0]));
+    CK(hipEventRecord(b, c.s[0]));
+    CK(hipEventSynchronize(b));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, a, b));
+    CK(hipGraphExecDestroy(ge));
+    CK(hipGraphDestroy(g));
+    CK(hipEventDestroy(a));
+    CK(hipEventDestroy(b));
+    return ms * 1000.f / (reps * B);   // us per batch
+}
+
+int main(int argc, char **argv) {
+    const int B = 64;
+    const size_t batch = 16u << 20;
+    uint32_t line_len = argc > 1 ? (uint32_t)atoi(argv[1]) : 64;
+    CK(hipSetDevice(0));
+    Ctx c;
+    for (int st = 0; st < kMaxS; ++st) {
+        if (c.ds[st].init(batch, 4) != 0) return 1;
+        CK(hipStreamCreateWithFlags(&c.s[st], hipStreamNonBlocking));
+        CK(hipEventCreateWithFlags(&c.join[st], hipEventDisableTiming));
+    }
+    CK(hipEventCreateWithFlags(&c.fork, hipEventDisableTiming));
+    std::vector<uint8_t> host(batch);
+    std::vector<size_t> lines;
+    for (int b = 0; b < B; ++b) {
+        size_t nd = 0, nl = 0;
+        const size_t n = sr_gen_stream(0x5EED0002ull + 65537ull * b, 0, &line_len, 1, 0.0, 4095, host.data(), batch,
+                                       nullptr, 0, &nd, &nl);
+        uint8_t *d;
+        CK(hipMalloc(&d, batch));
+        CK(hipMemcpy(d, host.data(), n, hipMemcpyHostToDevice));
+        c.batches.push_back(d);
+        c.sizes.push_back(n);
+        lines.push_back(nl);
+    }
+    c.max_lines = lines[0];
+    for (int st = 0; st < kMaxS; ++st) CK(hipMalloc(&c.d_out[st], c.max_lines * sizeof(sr_record)));
+    CK(hipMalloc(&c.d_n, B * sizeof(uint64_t)));
+    CK(hipMalloc(&c.sink, 4));
+
+    struct Row {
+        std::string name;
+        float us[3];
+    };
+    std::vector<Row> rows;
+    const int reps = 8;
+    for (int round = 0; round < 3; ++round) {
+        int i = 0;
+        auto put = [&](const char *name, float us) {
+            if (round == 0) rows.push_back(Row{name, {0, 0, 0}});
+            rows[i++].us[round] = us;
+        };
+        put("b1024_full_s1", time_variant<1024, ABL_NONE>(c, 1, reps));
+        put("b512_full_s1", time_variant<512, ABL_NONE>(c, 1, reps));
+        put("b256_full_s1", time_variant<256, ABL_NONE>(c, 1, reps));
+        put("b1024_full_s2", time_variant<1024, ABL_NONE>(c, 2, reps));
+        put("b512_full_s2", time_variant<512, ABL_NONE>(c, 2, reps));
+        put("b512_full_s4", time_variant<512, ABL_NONE>(c, 4, reps));
+        put("b256_full_s4", time_variant<256, ABL_NONE>(c, 4, reps));
+        put("b1024_no_lookback", time_variant<1024, ABL_NO_LOOKBACK>(c, 1, reps));
+        put("b1024_no_lines", time_variant<1024, ABL_NO_LINES>(c, 1, reps));
+        put("b1024_no_prologue", time_variant<1024, ABL_NO_PROLOGUE>(c, 1, reps));
+        put("b1024_no_lines_no_lookback", time_variant<1024, ABL_NO_LINES | ABL_NO_LOOKBACK>(c, 1, reps));
+        put("b1024_counts_only", time_variant<1024, ABL_NO_SCAN | ABL_NO_LINES | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps));
+        put("b1024_load_only", time_variant<1024, ABL_LOAD_ONLY | ABL_NO_LINES | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps));
+        put("read_kernel_s1", time_variant<256, 0xFFFFu>(c, 1, reps));
+        put("read_kernel_s4", time_variant<256, 0xFFFFu>(c, 4, reps));
+    }
+    // correctness: each product-shaped variant's line count on batch 0
+    {
+        uint64_t n = 0;
+        const RouteParams p = c.ds[0].params(c.batches[0], c.sizes[0], c.d_out[0], c.max_lines, nullptr, c.d_n);
+        launch_route<1024, ABL_NONE>(c.ds[0], p, c.s[0]);
+        CK(hipMemcpyAsync(&n, c.d_n, 8, hipMemcpyDeviceToHost, c.s[0]));
+        CK(hipStreamSynchronize(c.s[0]));
+        fprintf(stderr, "b1024 lines %llu expected %zu\n", (unsigned long long)n, lines[0]);
+        launch_route<256, ABL_NONE>(c.ds[0], p, c.s[0]);
+        CK(hipMemcpyAsync(&n, c.d_n, 8, hipMemcpyDeviceToHost, c.s[0]));
+        CK(hipStreamSynchronize(c.s[0]));
+        fprintf(stderr, "b256 lines %llu expected %zu\n", (unsigned long long)n, lines[0]);
+    }
+    printf("{\"line_len\": %u, \"batch_bytes\": %zu, \"us_per_batch\": {", line_len, batch);
+    for (size_t r = 0; r < rows.size(); ++r) {
+        float best = 1e9f;
+        for (int k = 0; k < 3; ++k) best = fminf(best, rows[r].us[k]);
+        printf("%s\"%s\": [%.2f, %.0f]", r ? ", " : "", rows[r].name.c_str(), best, batch / (best * 1e-6) / 1e9);
+    }
+    printf("}}\n");
+    return 0;
+}
