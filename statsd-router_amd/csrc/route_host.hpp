@@ -160,6 +160,7 @@ struct DeviceState {
         p.ctl = d_ctl;
         p.status = d_status;
         p.pending = d_pending;
+        p.dbg = nullptr;
         return p;
     }
 

@@ -33,9 +33,9 @@
 //     the reference's probe with a 16-entry register overlay of the permutation (each dead shard
 //     is probed at most once per line). Lines needing more than 16 dead probes are deferred to
 //     probe_wide_kernel (the probe on a full LDS permutation).
-//   * The last workgroup out (8-way sharded arrival counters) advances the context's epoch, so
-//     stale look-back granules of earlier launches are never mistaken for current ones, with or
-//     without graph replay.
+//   * Every workgroup arrives on 8-way sharded counters without waiting; the last tile waits for
+//     all arrivals and advances the context's epoch, so stale look-back granules of earlier
+//     launches are never mistaken for current ones, with or without graph replay.
 // No MFMA: HBM-bound byte work on VALU + LDS.
 #pragma once
 
@@ -65,6 +65,7 @@ enum : unsigned {
     ABL_NO_PROLOGUE = 4u,   // skip the straddling-line prologue
     ABL_NO_SCAN = 8u,       // skip masks/Horner/scans (counts only)
     ABL_LOAD_ONLY = 16u,    // load the tile into LDS and count '\n' only
+    ABL_STAMPS = 32u,       // diagnostic: s_memrealtime at phase boundaries into RouteParams::dbg
 };
 
 constexpr uint64_t ipow(uint64_t b, unsigned e) {
@@ -104,7 +105,7 @@ struct PendingLine {
 // Per-context device control block, zeroed once at sr_open. Counters on separate 128-B lines.
 struct Control {
     uint32_t epoch;
-    uint32_t top;
+    uint32_t pad1;
     uint32_t pending;
     uint32_t pad0[29];
     uint32_t done[8][32];
@@ -128,6 +129,7 @@ struct RouteParams {
     Control *ctl;
     uint64_t *status;        // per-tile look-back granules
     PendingLine *pending;
+    uint64_t *dbg;           // ABL_STAMPS builds only: 8 timestamps per tile
 };
 
 // ---------------------------------------------------------------------------------------
@@ -239,10 +241,56 @@ __device__ __forceinline__ int wave_max_i32(int v) {
     return v;
 }
 
+// ---- DPP wave primitives (GFX9 row_shr / row_bcast / wave_shr; no LDS round trip) ----------
+constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
+constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143, kDppWaveShr1 = 0x138;
+
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint32_t dpp32(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROW_MASK, 0xF, false);
+}
+
+template <int CTRL, int ROW_MASK = 0xF>
+__device__ __forceinline__ uint64_t dpp64(uint64_t old, uint64_t v) {
+    const uint32_t lo = dpp32<CTRL, ROW_MASK>((uint32_t)old, (uint32_t)v);
+    const uint32_t hi = dpp32<CTRL, ROW_MASK>((uint32_t)(old >> 32), (uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Inclusive wave64 scan with an associative combine f(left, right) and identity id.
+template <class F>
+__device__ __forceinline__ uint64_t wave_scan64(uint64_t v, uint64_t id, F f) {
+    v = f(dpp64<kDppRowShr1>(id, v), v);
+    v = f(dpp64<kDppRowShr2>(id, v), v);
+    v = f(dpp64<kDppRowShr4>(id, v), v);
+    v = f(dpp64<kDppRowShr8>(id, v), v);
+    v = f(dpp64<kDppRowBcast15, 0xA>(id, v), v);
+    v = f(dpp64<kDppRowBcast31, 0xC>(id, v), v);
+    return v;
+}
+
+// value of the lane below (lane 0: id)
+__device__ __forceinline__ uint64_t wave_shr1_64(uint64_t v, uint64_t id) { return dpp64<kDppWaveShr1>(id, v); }
+
+__device__ __forceinline__ uint32_t wave_add32(uint32_t v) {   // sum over the wave, in every lane
+    v += dpp32<kDppRowShr1>(0u, v);
+    v += dpp32<kDppRowShr2>(0u, v);
+    v += dpp32<kDppRowShr4>(0u, v);
+    v += dpp32<kDppRowShr8>(0u, v);
+    v += dpp32<kDppRowBcast15, 0xA>(0u, v);
+    v += dpp32<kDppRowBcast31, 0xC>(0u, v);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
     const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
     return ((uint64_t)hi << 32) | lo;
+}
+
+template <unsigned ABL>
+__device__ __forceinline__ void stamp(const RouteParams &p, int tid, uint32_t t, int slot) {
+    if ((ABL & ABL_STAMPS) && tid == 0) p.dbg[(size_t)t * 8 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Segmented "line state" scan element: [63:32] newline count, [31] lane range holds a '\n',
@@ -311,20 +359,22 @@ template <int BLOCK>
 struct SmemT {
     static constexpr int kWaves = BLOCK / 64;
     static constexpr int kTileB = BLOCK * kLaneBytes;
-    static constexpr int kPiecesB = kTileB / 16;
-    static constexpr int kWin = BLOCK >= 512 ? 2048 : 1024;   // tile-local lines staged per round
-    uint4 tile[kPiecesB];            // the tile's bytes
-    uint64_t pstate[kPiecesB];       // P(16p - 1) for every 16-byte piece p (tile frame, P(-1)=0)
-    uint32_t lend[kWin + 1];         // per staged line: position of its '\n'; slot 0 = previous line
-    int32_t lcol[kWin + 1];          // per staged line: first ':' (kNone if none; < 0: before the tile)
+    static constexpr int kHalo = 2048;                // bytes before the tile kept in LDS
+    static constexpr int kWin = 2 * BLOCK;            // tile-local lines staged per round
+    // LDS image of the batch bytes [T0 - kHalo, T0 + tile): 64-byte rows stored as 17 dwords (one
+    // pad dword per row) so that lanes reading at 64-byte strides hit distinct banks.
+    static constexpr int kRows = (kHalo + kTileB) / 64;
+    static constexpr int kWords = kRows * 17 + 20;
+    uint32_t img[kWords];
+    int32_t lend[kWin + 1];          // per staged line: tile position of its '\n'; slot 0 = previous
+    int32_t lcol[kWin + 1];          // per staged line: first ':' in the tile part (kNone if none)
     uint64_t wave_seg[kWaves];
-    uint64_t wave_hash[kWaves];
+    uint64_t wave_pre[kWaves];       // exclusive line state of each wave
     uint32_t wave_cnt[kWaves];
     uint64_t kp_lo[64];              // K^i
     uint64_t kp_hi[64];              // K^(64 i)
     uint64_t kinv[64];               // K^-i
-    uint64_t h_pre, hc_pre;          // straddling line: Horner of [s_pre, 0) and [s_pre, c_pre)
-    int32_t s_pre, c_pre;            // tile-relative start / first colon (c_pre: kNone if none)
+    int32_t s_pre, c_pre;            // straddling line: tile-relative start / first colon before T0
     uint32_t epoch, base;
 };
 
@@ -334,14 +384,49 @@ __device__ __forceinline__ uint64_t kpow_n(const S &sm, int n) {
     return sm.kp_hi[n >> 6] * sm.kp_lo[n & 63];
 }
 
-// P(x) in the tile frame for -1 <= x < tile: Horner of tile bytes [0, x].
+// dword index in the padded LDS image of image byte b (b % 4 == 0 for whole dwords)
+__device__ __forceinline__ int img_dw(int b) { return (b >> 6) * 17 + ((b >> 2) & 15); }
+
+// sdbm (Horner, no colon test) of the n <= 64 image bytes starting at image byte a.
+// Aligned dword reads + v_alignbyte; whole dwords by sdbm_dword, the tail through the
+// zero-padding identity Horner(x, 0^z) = Horner(x) * K^z.
 template <class S>
-__device__ __forceinline__ uint64_t prefix_at(const S &sm, int x) {
-    if (x < 0) return 0;
-    const int pc = x >> 4, r = x & 15;
-    const uint64_t t = sdbm_piece(sm.tile[pc], 0, r + 1);
-    // t = Horner(bytes[16pc .. x]) * K^(15 - r); undo the trailing zeros with K^-1.
-    return sm.pstate[pc] * sm.kp_lo[r + 1] + t * sm.kinv[15 - r];
+__device__ __forceinline__ uint64_t sdbm_lds(const S &sm, int a, int n) {
+    const int base = a & ~3, sh = a & 3;
+    const int i0 = img_dw(base), r0 = base & 63;
+    const int nfull = n >> 2, rem = n & 3;
+    uint32_t w[17];
+#pragma unroll
+    for (int m = 0; m < 17; ++m) w[m] = sm.img[i0 + m + ((r0 + 4 * m) >> 6)];
+    uint64_t h = 0;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        if (m < nfull) h = sdbm_dword(h, __builtin_amdgcn_alignbyte(w[m + 1], w[m], sh));
+    }
+    if (rem) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+            if (m == nfull) x = __builtin_amdgcn_alignbyte(w[m + 1], w[m], sh);
+        x &= (1u << (8 * rem)) - 1u;
+        h = sdbm_dword(h, x) * sm.kinv[4 - rem];
+    }
+    return h;
+}
+
+// store / load one 16-byte chunk at image byte b (b % 16 == 0: never crosses a row)
+template <class S>
+__device__ __forceinline__ void img_put16(S &sm, int b, uint4 v) {
+    const int i = img_dw(b);
+    sm.img[i] = v.x;
+    sm.img[i + 1] = v.y;
+    sm.img[i + 2] = v.z;
+    sm.img[i + 3] = v.w;
+}
+template <class S>
+__device__ __forceinline__ uint4 img_get16(const S &sm, int b) {
+    const int i = img_dw(b);
+    return make_uint4(sm.img[i], sm.img[i + 1], sm.img[i + 2], sm.img[i + 3]);
 }
 
 // Number of '\n' bytes in tile m, counted by one wave (only used when a predecessor has not
@@ -360,22 +445,38 @@ __device__ uint32_t count_tile_wave(const RouteParams &p, __amdgpu_buffer_rsrc_t
 
 // Exclusive line prefix of tile t: decoupled look-back by ONE wave,
 // 256 predecessors per round, stopping at the nearest inclusive prefix. Every lane returns the same value.
+constexpr int kLookPer = 4;   // predecessors per lane per look-back round
+
+// First round of status loads, issued early so their latency hides behind the mask pass.
+__device__ __forceinline__ void look_back_prefetch(const RouteParams &p, uint32_t t, int lane,
+                                                   uint64_t (&first)[kLookPer]) {
+#pragma unroll
+    for (int k = 0; k < kLookPer; ++k) {
+        const int64_t idx = (int64_t)t - 1 - lane - 64 * k;
+        first[k] = idx >= 0 ? __hip_atomic_load(&p.status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    }
+}
+
 template <int BLOCK>
 __device__ uint32_t look_back_wave(const RouteParams &p, __amdgpu_buffer_rsrc_t rsrc, uint32_t t, uint32_t epoch,
-                                   int lane) {
-    constexpr int kPer = 4;
+                                   int lane, const uint64_t (&first)[kLookPer]) {
+    constexpr int kPer = kLookPer;
     uint64_t acc = 0;
     int64_t hi = t;
     const uint32_t ep = epoch & 0x3FFFFFFFu;
+    bool round0 = true;
     while (hi > 0) {
         const int64_t lo = hi - 64 * kPer > 0 ? hi - 64 * kPer : 0;
         uint64_t st[kPer];
         bool need[kPer];
 #pragma unroll
         for (int k = 0; k < kPer; ++k) {
-            need[k] = hi - 1 - lane - 64 * k >= lo;
-            st[k] = 0;
+            const bool in = hi - 1 - lane - 64 * k >= lo;
+            st[k] = round0 ? first[k] : 0ull;
+            need[k] = in && !((uint32_t)(st[k] >> 34) == ep && ((st[k] >> 32) & 3u) != 0);
         }
+        round0 = false;
+        if (!__ballot(need[0] | need[1] | need[2] | need[3])) goto polled;
         for (int spin = 0;; ++spin) {
             bool pending = false;
 #pragma unroll
@@ -390,6 +491,7 @@ __device__ uint32_t look_back_wave(const RouteParams &p, __amdgpu_buffer_rsrc_t 
             if (spin >= kSpinBudget) break;
             __builtin_amdgcn_s_sleep(2);
         }
+    polled:
         // predecessors still silent: count their tiles here (never needed under in-order
         // dispatch; it makes progress independent of dispatch order)
 #pragma unroll
@@ -426,13 +528,21 @@ __device__ uint32_t look_back_wave(const RouteParams &p, __amdgpu_buffer_rsrc_t 
     return (uint32_t)acc;
 }
 
+template <int BLOCK>
+struct KernelTraits {
+    // waves per SIMD to reserve registers for: 1024-thread tiles run one workgroup per CU,
+    // smaller tiles several (LDS: 86 KB / 45 KB / 24 KB per workgroup)
+    static constexpr int kMinWavesPerSimd = BLOCK >= 1024 ? 4 : 6;
+};
+
 template <int BLOCK, unsigned ABL>
-__global__ __launch_bounds__(BLOCK, 4) void route_kernel(RouteParams p) {
+__global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void route_kernel(RouteParams p) {
     using S = SmemT<BLOCK>;
     constexpr int kWaves = S::kWaves;
     constexpr int kTileB = S::kTileB;
+    constexpr int kHalo = S::kHalo;
     constexpr int kWin = S::kWin;
-    constexpr int kPreWave = kWaves - 1;   // the wave that finishes the straddling line
+    constexpr int kPreWave = kWaves - 1;   // the wave that locates the straddling line
     __shared__ S sm;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -442,12 +552,16 @@ __global__ __launch_bounds__(BLOCK, 4) void route_kernel(RouteParams p) {
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)p.bytes, (short)0, (int)p.nbytes, 0x00020000);
 
+    stamp<ABL>(p, tid, t, 0);
     if (tid == 0) sm.epoch = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < kPowTable) (&sm.kp_lo[0])[tid] = p.kpow[tid];   // kp_lo | kp_hi | kinv are contiguous
-    // the 1 KiB before the tile (straddling line), issued together with the tile loads
-    uint4 pre0 = make_uint4(0, 0, 0, 0);
-    if (!(ABL & ABL_NO_PROLOGUE) && wave == kPreWave && t > 0)
-        pre0 = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)(T0 - 1024) + lane * 16, 0, 0));
+    if (tid < kHalo / 16) {   // the 2 KiB before the tile (zeros before the batch start)
+        uint4 hv = make_uint4(0, 0, 0, 0);
+        if (t > 0 && !(ABL & ABL_NO_PROLOGUE))
+            hv = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)(T0 - kHalo) + tid * 16, 0, 0));
+        img_put16(sm, tid * 16, hv);
+    }
+    if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
     // coalesced tile load: wave instruction k of thread tid covers bytes k*BLOCK*16 + tid*16;
     // the '\n' count is taken from the registers so the tile's aggregate can be published early
     {
@@ -457,14 +571,15 @@ __global__ __launch_bounds__(BLOCK, 4) void route_kernel(RouteParams p) {
         for (int k = 0; k < 4; ++k) v[k] = load16(rsrc, (uint32_t)T0 + k * BLOCK * 16 + tid * 16, p.nbytes);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            sm.tile[k * BLOCK + tid] = v[k];
+            img_put16(sm, kHalo + 16 * (k * BLOCK + tid), v[k]);
             cnt += eq_count4(v[k].x, 0x0A0A0A0Au) + eq_count4(v[k].y, 0x0A0A0A0Au) +
                    eq_count4(v[k].z, 0x0A0A0A0Au) + eq_count4(v[k].w, 0x0A0A0A0Au);
         }
-        cnt = (uint32_t)wave_sum64(cnt);
+        cnt = wave_add32(cnt);
         if (lane == 0) sm.wave_cnt[wave] = cnt;
     }
     __syncthreads();
+    stamp<ABL>(p, tid, t, 1);
     const uint32_t epoch = sm.epoch;
     uint32_t tile_count = 0;
 #pragma unroll
@@ -473,107 +588,24 @@ __global__ __launch_bounds__(BLOCK, 4) void route_kernel(RouteParams p) {
         const uint64_t st = mk_status(epoch, t == 0 ? kFlagIncl : kFlagAgg, tile_count);
         __hip_atomic_store(&p.status[t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-
-    // ---- one wave: the line that straddles into this tile (starts before T0) ------------------
-    if (wave == kPreWave && !(ABL & ABL_NO_PROLOGUE)) {
-        int64_t s_abs = 0;
-        if (t > 0) {
-            uint32_t nl16 = eq_mask16(pre0, 0x0A0A0A0Au);
-            uint64_t m = __ballot(nl16 != 0);
-            int64_t a = T0 - 1024 + lane * 16;
-            if (!m) {   // line longer than 1 KiB: keep searching backwards
-                int64_t hi = T0 - 1024;
-                while (hi > 0 && !m) {
-                    const int64_t lo = hi - 1024 > 0 ? hi - 1024 : 0;
-                    a = lo + lane * 16;
-                    nl16 = 0;
-                    if (a < hi) nl16 = eq_mask16(load16(rsrc, (uint32_t)a, p.nbytes), 0x0A0A0A0Au);
-                    m = __ballot(nl16 != 0);
-                    hi = lo;
-                }
-            }
-            if (m) {
-                const int L = 63 - __builtin_clzll(m);
-                const int64_t last = a + 31 - __builtin_clz(nl16 | 1u);   // valid on lane L
-                s_abs = (int64_t)readlane64((uint64_t)last, L) + 1;
-            }
-        }
-        const int32_t s_pre = (int32_t)(s_abs - T0);
-        uint64_t h_pre = 0, hc_pre = 0;
-        int32_t c_pre = kNone;
-        if (s_pre < 0 && -s_pre <= (int)SR_MAX_LINE_LENGTH - 1) {
-            // windows of 64 pieces: w = 1 is [T0-2048, T0-1024) (only for lines over 1 KiB)
-            const int nwin = -s_pre > 1024 ? 2 : 1;
-            uint4 pw[2];
-            pw[0] = pre0;
-            pw[1] = nwin == 2 ? load16(rsrc, (uint32_t)(T0 - 2048) + lane * 16, p.nbytes) : make_uint4(0, 0, 0, 0);
-            // first colon at or after s_abs, oldest window first
-            int64_t cabs = -1;
-#pragma unroll
-            for (int w = 1; w >= 0; --w) {
-                if (w >= nwin || cabs >= 0) continue;
-                const int64_t pb = T0 - 1024 * (w + 1) + lane * 16;
-                const int skip = (int)max<int64_t>(0, min<int64_t>(16, s_abs - pb));
-                const uint32_t cm = eq_mask16(pw[w], 0x3A3A3A3Au) & (0xFFFFu << skip) & 0xFFFFu;
-                const uint64_t cb = __ballot(cm != 0);
-                if (cb) {
-                    const int lc = __builtin_ctzll(cb);
-                    cabs = (int64_t)readlane64((uint64_t)(pb + __builtin_ctz(cm | 0x10000u)), lc);
-                }
-            }
-            uint64_t hs = 0, hcs = 0;
-#pragma unroll
-            for (int w = 0; w < 2; ++w) {
-                if (w >= nwin) continue;
-                const int64_t pb = T0 - 1024 * (w + 1) + lane * 16, pe = pb + 16;
-                const int skip = (int)max<int64_t>(0, min<int64_t>(16, s_abs - pb));
-                const uint64_t qv = sdbm_piece(pw[w], skip, 16);
-                hs += qv * kpow_n(sm, (int)(T0 - pe));
-                if (cabs >= 0) {
-                    if (pe <= cabs) hcs += qv * kpow_n(sm, (int)(cabs - pe));
-                    else if (pb < cabs) hcs += sdbm_piece(pw[w], skip, (int)(cabs - pb)) * sm.kinv[pe - cabs];
-                }
-            }
-            h_pre = wave_sum64(hs);
-            if (cabs >= 0) {
-                c_pre = (int32_t)(cabs - T0);
-                hc_pre = wave_sum64(hcs);
-            }
-        }
-        if (lane == 0) {
-            sm.s_pre = s_pre;
-            sm.c_pre = c_pre;
-            sm.h_pre = h_pre;
-            sm.hc_pre = hc_pre;
-        }
-    } else if ((ABL & ABL_NO_PROLOGUE) && tid == 0) {
-        sm.s_pre = 0;
-        sm.c_pre = kNone;
-        sm.h_pre = sm.hc_pre = 0;
-    }
-
-    // ---- per lane: 64 contiguous bytes ---------------------------------------------------------
+    uint64_t lb_first[kLookPer] = {0ull, 0ull, 0ull, 0ull};
+    if (wave == 0 && !(ABL & ABL_NO_LOOKBACK)) look_back_prefetch(p, t, lane, lb_first);
+    if (ABL & ABL_LOAD_ONLY) {
+        if (tid == 0 && t == p.ntiles - 1) *p.n_out = tile_count;
+        __syncthreads();
+    } else {
+    // ---- per lane: '\n' / ':' masks of its 64 contiguous bytes, segmented line-state scan -------
     const int o = tid * kLaneBytes;   // tile position of the lane's first byte
     uint64_t nlm = 0, clm = 0;        // bit i: byte o+i is '\n' / ':'
-    uint64_t q = 0, q16 = 0, q32 = 0, q48 = 0;
-    if (ABL & (ABL_LOAD_ONLY | ABL_NO_SCAN)) {
 #pragma unroll
-        for (int pc = 0; pc < 4; ++pc) nlm |= (uint64_t)eq_mask16(sm.tile[tid * 4 + pc], 0x0A0A0A0Au) << (16 * pc);
-    } else {
+    for (int pc = 0; pc < 4; ++pc) {
+        const uint4 v = img_get16(sm, kHalo + 64 * tid + 16 * pc);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int pc = 0; pc < 4; ++pc) {
-            const uint4 v = sm.tile[tid * 4 + pc];
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int sh = 16 * pc + 4 * k;
-                nlm |= (uint64_t)eq_mask4(w[k], 0x0A0A0A0Au) << sh;
-                clm |= (uint64_t)eq_mask4(w[k], 0x3A3A3A3Au) << sh;
-                q = sdbm_dword(q, w[k]);
-            }
-            if (pc == 0) q16 = q;
-            if (pc == 1) q32 = q;
-            if (pc == 2) q48 = q;
+        for (int k = 0; k < 4; ++k) {
+            const int sh = 16 * pc + 4 * k;
+            nlm |= (uint64_t)eq_mask4(w[k], 0x0A0A0A0Au) << sh;
+            clm |= (uint64_t)eq_mask4(w[k], 0x3A3A3A3Au) << sh;
         }
     }
     const int ncnt = __popcll(nlm);
@@ -586,55 +618,25 @@ __global__ __launch_bounds__(BLOCK, 4) void route_kernel(RouteParams p) {
     } else {
         seg = clm ? (uint32_t)(o + __builtin_ctzll(clm)) : (uint32_t)kNone;
     }
-    // wave inclusive scans: seg (line state) and q (Horner, multiplier K^64 per lane)
-    uint64_t sseg = seg, shash = q;
-    if (!(ABL & ABL_LOAD_ONLY)) {
-        uint64_t mul = kK64;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t a = shfl_up64(sseg, d);
-            const uint64_t b = shfl_up64(shash, d);
-            if (lane >= d) {
-                sseg = seg_combine(a, sseg);
-                shash = b * mul + shash;
-            }
-            mul *= mul;
-        }
-    }
-    if (lane == 63) {
-        sm.wave_seg[wave] = sseg;
-        sm.wave_hash[wave] = shash;
+    auto comb = [](uint64_t f, uint64_t g) { return seg_combine(f, g); };
+    const uint64_t sseg = wave_scan64(seg, (uint64_t)kNone, comb);
+    if (lane == 63) sm.wave_seg[wave] = sseg;
+    __syncthreads();
+    stamp<ABL>(p, tid, t, 2);
+    if (wave == 0) {   // exclusive line state of every wave
+        const uint64_t v = wave_scan64(lane < kWaves ? sm.wave_seg[lane] : (uint64_t)kNone, (uint64_t)kNone, comb);
+        const uint64_t ex = wave_shr1_64(v, (uint64_t)kNone);
+        if (lane < kWaves) sm.wave_pre[lane] = ex;
     }
     __syncthreads();
-    uint64_t eseg = shfl_up64(sseg, 1);
-    uint64_t ehash = shfl_up64(shash, 1);
-    if (lane == 0) {
-        eseg = (uint64_t)kNone;   // empty range: count 0, no '\n', no colon
-        ehash = 0;
-    }
-    {
-        uint64_t cseg = (uint64_t)kNone, chash = 0;   // carry of the waves before this one
-        for (int w2 = 0; w2 < wave; ++w2) {
-            cseg = seg_combine(cseg, sm.wave_seg[w2]);
-            chash = chash * kK4096 + sm.wave_hash[w2];
-        }
-        eseg = seg_combine(cseg, eseg);
-        ehash = chash * sm.kp_hi[lane] + ehash;
-    }
-    if (!(ABL & ABL_LOAD_ONLY)) {
-        sm.pstate[tid * 4 + 0] = ehash;
-        sm.pstate[tid * 4 + 1] = ehash * kK16 + q16;
-        sm.pstate[tid * 4 + 2] = ehash * kK32 + q32;
-        sm.pstate[tid * 4 + 3] = ehash * kK48 + q48;
-    }
-    const int s_pre = sm.s_pre;
-    const int c_pre = sm.c_pre;
+    // empty range (lane 0): count 0, no '\n', no colon
+    const uint64_t eseg = seg_combine(sm.wave_pre[wave], wave_shr1_64(sseg, (uint64_t)kNone));
 
-    // ---- wave 0: decoupled look-back (the other waves stage their lines meanwhile) ------------
+    // ---- wave 0: decoupled look-back for the tile's first record index -----------------------
     if (wave == 0) {
         uint32_t base = 0;
         if (!(ABL & ABL_NO_LOOKBACK)) {
-            base = look_back_wave<BLOCK>(p, rsrc, t, epoch, lane);
+            base = look_back_wave<BLOCK>(p, rsrc, t, epoch, lane, lb_first);
             if (lane == 0 && t > 0) {
                 const uint64_t st = mk_status(epoch, kFlagIncl, base + tile_count);
                 __hip_atomic_store(&p.status[t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -644,100 +646,166 @@ __global__ __launch_bounds__(BLOCK, 4) void route_kernel(RouteParams p) {
             sm.base = base;
             if (t == p.ntiles - 1) *p.n_out = (uint64_t)base + tile_count;
         }
+        stamp<ABL>(p, tid, t, 3);
+    }
+    // ---- last wave: where the line that straddles into the tile starts, its first ':' ----------
+    if (wave == kPreWave) {
+        int64_t s_abs = 0;
+        int32_t c_pre = kNone;
+        if (t > 0 && !(ABL & ABL_NO_PROLOGUE)) {
+            // the halo: lane l looks at LDS bytes [32l, 32l + 32) = positions T0 - 2048 + 32l ...
+            const uint4 a0 = img_get16(sm, 32 * lane), a1 = img_get16(sm, 32 * lane + 16);
+            const uint32_t nl32 = eq_mask16(a0, 0x0A0A0A0Au) | (eq_mask16(a1, 0x0A0A0A0Au) << 16);
+            const uint64_t m = __ballot(nl32 != 0);
+            if (m) {
+                const int L = 63 - __builtin_clzll(m);
+                const int pos = (int)__builtin_amdgcn_readlane(32 * lane + 31 - __builtin_clz(nl32 | 1u), L);
+                s_abs = T0 - kHalo + pos + 1;
+            } else {   // a line longer than the halo (necessarily invalid): find its exact start
+                int64_t hi = T0 - kHalo;
+                uint64_t mm = 0;
+                int64_t a = 0;
+                uint32_t nl16 = 0;
+                while (hi > 0 && !mm) {
+                    const int64_t lo = hi - 1024 > 0 ? hi - 1024 : 0;
+                    a = lo + lane * 16;
+                    nl16 = 0;
+                    if (a < hi) nl16 = eq_mask16(load16(rsrc, (uint32_t)a, p.nbytes), 0x0A0A0A0Au);
+                    mm = __ballot(nl16 != 0);
+                    hi = lo;
+                }
+                if (mm) {
+                    const int L = 63 - __builtin_clzll(mm);
+                    s_abs = (int64_t)readlane64((uint64_t)(a + 31 - __builtin_clz(nl16 | 1u)), L) + 1;
+                }
+            }
+            const int s_rel = (int)(s_abs - T0);
+            if (s_rel < 0 && -s_rel <= (int)SR_MAX_LINE_LENGTH - 1) {   // could be valid: first ':' before T0
+                const int b0 = kHalo + s_rel - 32 * lane;   // first LDS byte of the line within my 32
+                const uint32_t keep = b0 <= 0 ? 0xFFFFFFFFu : (b0 >= 32 ? 0u : ~((1u << b0) - 1u));
+                const uint32_t cm = (eq_mask16(a0, 0x3A3A3A3Au) | (eq_mask16(a1, 0x3A3A3A3Au) << 16)) & keep;
+                const uint64_t cb = __ballot(cm != 0);
+                if (cb) {
+                    const int L = __builtin_ctzll(cb);
+                    const int pos = (int)__builtin_amdgcn_readlane(32 * lane + __builtin_ctz(cm | 0x80000000u), L);
+                    c_pre = pos - kHalo;
+                }
+            }
+        }
+        if (lane == 0) {
+            sm.s_pre = (int32_t)(s_abs - T0);
+            sm.c_pre = c_pre;
+        }
     }
 
-    // ---- per line: windows of kWin tile-local lines ----------------------------------------------
-    if (!(ABL & (ABL_NO_LINES | ABL_LOAD_ONLY))) {
-        const int lane_first = (int)(eseg >> 32);               // tile-local index of lane's 1st line
-        const bool open_has_nl = (uint32_t)eseg & 0x80000000u;  // a '\n' earlier in the tile
-        int open_fc = (int)((uint32_t)eseg & 0x1FFFFu);         // first ':' of the open line
-        if (!open_has_nl && c_pre != kNone) open_fc = c_pre;    // straddling line: colon before T0
-        if (tid == 0) sm.lend[0] = 0;
-        for (int wbase = 0; wbase < (int)tile_count; wbase += kWin) {
-            // (1) stage (e, c) of the lane's lines that fall into this window
-            if (nlm && lane_first + ncnt > wbase && lane_first < wbase + kWin) {
-                uint64_t m = nlm;
-                int idx = lane_first;
-                int prevb = -1;
-                while (m) {
-                    const int b = __builtin_ctzll(m);
-                    m &= m - 1;
-                    int c;
-                    if (prevb < 0 && open_fc != kNone) {
-                        c = open_fc;
-                    } else {
-                        const uint64_t below = b == 0 ? 0ull : (~0ull >> (64 - b));
-                        const uint64_t above = ~0ull << (prevb + 1);
-                        const uint64_t cm = clm & below & above;
-                        c = cm ? o + __builtin_ctzll(cm) : kNone;
-                    }
-                    if (idx >= wbase && idx < wbase + kWin) {
-                        sm.lend[idx - wbase + 1] = (uint32_t)(o + b);
-                        sm.lcol[idx - wbase + 1] = c;
-                    }
-                    ++idx;
-                    prevb = b;
-                }
-            }
-            __syncthreads();
-            const uint32_t base = sm.base;
-            // (2) one thread per line
-            const int nwin = min(kWin, (int)tile_count - wbase);
-            for (int jj = tid; jj < nwin; jj += BLOCK) {
-                const int j = wbase + jj;
-                const int e = (int)sm.lend[jj + 1];
-                const int c = sm.lcol[jj + 1];
-                const int s = (j == 0) ? s_pre : (int)sm.lend[jj] + 1;
-                const int64_t len = (int64_t)e - s + 1;
-                uint32_t route;
-                uint64_t h = 0;
-                if (len < (int)SR_MIN_LINE_LENGTH || len > (int)SR_MAX_LINE_LENGTH) {   // sr-main.c:180
-                    route = SR_ROUTE_INVALID_LENGTH;
-                } else if (c == kNone || c > e) {                                        // sr-main.c:140
-                    route = SR_ROUTE_INVALID_FORMAT;
+    // ---- per line: windows of kWin tile-local lines ------------------------------------------
+    const int lane_first = (int)(eseg >> 32);               // tile-local index of lane's 1st line
+    const int open_fc = (int)((uint32_t)eseg & 0x1FFFFu);   // first ':' (in the tile) of the open line
+    if (tid == 0) sm.lend[0] = 0;
+    for (int wbase = 0; wbase < (int)tile_count; wbase += kWin) {
+        // (1) stage (e, c) of the lane's lines that fall into this window
+        if (nlm && lane_first + ncnt > wbase && lane_first < wbase + kWin) {
+            uint64_t m = nlm;
+            int idx = lane_first;
+            int prevb = -1;
+            while (m) {
+                const int b = __builtin_ctzll(m);
+                m &= m - 1;
+                int c;
+                if (prevb < 0 && open_fc != kNone) {
+                    c = open_fc;
                 } else {
-                    if (j == 0) {
-                        h = c < 0 ? sm.hc_pre : sm.h_pre * kpow_n(sm, c) + prefix_at(sm, c - 1);
-                    } else {
-                        h = prefix_at(sm, c - 1) - prefix_at(sm, s - 1) * kpow_n(sm, c - s);
-                    }
-                    route = probe_shard(h, p);
+                    const uint64_t below = b == 0 ? 0ull : (~0ull >> (64 - b));
+                    const uint64_t above = ~0ull << (prevb + 1);
+                    const uint64_t cm = clm & below & above;
+                    c = cm ? o + __builtin_ctzll(cm) : kNone;
                 }
-                const uint32_t rec = base + (uint32_t)j;
-                if (rec < p.max_records) {
-                    if (route == kRoutePending) {
-                        const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
-                        if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, 0u, h};
+                if (idx >= wbase && idx < wbase + kWin) {
+                    sm.lend[idx - wbase + 1] = o + b;
+                    sm.lcol[idx - wbase + 1] = c;
+                }
+                ++idx;
+                prevb = b;
+            }
+        }
+        __syncthreads();
+        if (wbase == 0) stamp<ABL>(p, tid, t, 4);
+        if (!(ABL & ABL_NO_LINES)) {
+            const uint32_t base = sm.base;
+            const int s_pre = sm.s_pre;
+            const int c_pre = sm.c_pre;
+            const int nwin = min(kWin, (int)tile_count - wbase);
+            // lanes per line from the mean line length: 64-byte hash segments per lane
+            const int mean = kTileB / max((int)tile_count, 1);
+            int G = 1;
+            while (G < 32 && G * 64 < mean) G <<= 1;
+            const int nG = BLOCK / G, gi = tid & (G - 1);
+            for (int jj = tid / G; jj < nwin; jj += nG) {
+                const int j = wbase + jj;
+                const int e = sm.lend[jj + 1];
+                int c = sm.lcol[jj + 1];
+                if (j == 0 && c_pre != kNone) c = c_pre;   // the straddling line's ':' lies before T0
+                const int s = (j == 0) ? s_pre : sm.lend[jj] + 1;
+                const int len = e - s + 1;
+                const bool len_ok = len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH;   // :180
+                const bool fmt_ok = c != kNone && c < e;                                                // :140
+                uint64_t h = 0;
+                if (len_ok && fmt_ok) {
+                    // sdbm of [s, c) = sum over 64-byte segments k of Horner(seg_k) * K^(c - end_k)
+                    const int n = c - s, nseg = (n + 63) >> 6;
+                    for (int k = gi; k < nseg; k += G) {
+                        const int a = s + 64 * k, nn = min(64, n - 64 * k);
+                        h += sdbm_lds(sm, a + kHalo, nn) * kpow_n(sm, c - a - nn);
                     }
-                    sr_record r;
-                    r.offset = (uint32_t)(T0 + s);
-                    r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
-                    r.route = (uint16_t)route;
-                    p.recs[rec] = r;
-                    if (p.hashes) p.hashes[rec] = h;
+                }
+                for (int d = G >> 1; d >= 1; d >>= 1) h += shfl_xor64(h, d);
+                if (gi == 0) {
+                    uint32_t route;
+                    if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
+                    else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
+                    else route = probe_shard(h, p);                                                    // :145
+                    const uint32_t rec = base + (uint32_t)j;
+                    if (rec < p.max_records) {
+                        if (route == kRoutePending) {
+                            const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
+                            if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, 0u, h};
+                        }
+                        sr_record r;
+                        r.offset = (uint32_t)(T0 + s);
+                        r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
+                        r.route = (uint16_t)route;
+                        p.recs[rec] = r;
+                        if (p.hashes) p.hashes[rec] = h;
+                    }
                 }
             }
-            __syncthreads();
-            if (tid == 0) sm.lend[0] = sm.lend[nwin];
-            __syncthreads();
         }
-    } else {
+        __syncthreads();
+        if (wbase == 0) stamp<ABL>(p, tid, t, 5);
+        if (tid == 0) sm.lend[0] = sm.lend[min(kWin, (int)tile_count - wbase)];
         __syncthreads();
     }
+    }
+    stamp<ABL>(p, tid, t, 6);
 
-    // ---- the last workgroup out advances the epoch (8-way sharded arrival counters) ----------
+    // ---- arrivals: every workgroup adds itself (no return value, nothing waits); the last tile
+    // waits until all have arrived, then resets the counters and advances the epoch. Every
+    // workgroup read the epoch before arriving, so none of this launch can see the new one.
     if (tid == 0) {
-        const uint32_t s = t & 7u;
-        const uint32_t cnt_s = (p.ntiles - s + 7u) / 8u;   // workgroups b < ntiles with b % 8 == s
-        const uint32_t old = atomicAdd(&p.ctl->done[s][0], 1u);
-        if (old == cnt_s - 1) {
-            __hip_atomic_store(&p.ctl->done[s][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t nsh = p.ntiles < 8 ? p.ntiles : 8u;
-            const uint32_t top = atomicAdd(&p.ctl->top, 1u);
-            if (top == nsh - 1) {
-                __hip_atomic_store(&p.ctl->top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&p.ctl->epoch, epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(&p.ctl->done[t & 7u][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t == p.ntiles - 1) {
+            for (uint32_t spin = 0; spin < (1u << 26); ++spin) {
+                uint32_t n = 0;
+#pragma unroll
+                for (int s8 = 0; s8 < 8; ++s8)
+                    n += __hip_atomic_load(&p.ctl->done[s8][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (n >= p.ntiles) break;
+                __builtin_amdgcn_s_sleep(2);
             }
+#pragma unroll
+            for (int s8 = 0; s8 < 8; ++s8)
+                __hip_atomic_store(&p.ctl->done[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&p.ctl->epoch, epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }

@@ -147,12 +147,12 @@ int main(int argc, char **argv) {
         put("b512_full_s2", time_variant<512, ABL_NONE>(c, 2, reps));
         put("b512_full_s4", time_variant<512, ABL_NONE>(c, 4, reps));
         put("b256_full_s4", time_variant<256, ABL_NONE>(c, 4, reps));
-        put("b1024_no_lookback", time_variant<1024, ABL_NO_LOOKBACK>(c, 1, reps));
-        put("b1024_no_lines", time_variant<1024, ABL_NO_LINES>(c, 1, reps));
-        put("b1024_no_prologue", time_variant<1024, ABL_NO_PROLOGUE>(c, 1, reps));
-        put("b1024_no_lines_no_lookback", time_variant<1024, ABL_NO_LINES | ABL_NO_LOOKBACK>(c, 1, reps));
-        put("b1024_counts_only", time_variant<1024, ABL_NO_SCAN | ABL_NO_LINES | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps));
-        put("b1024_load_only", time_variant<1024, ABL_LOAD_ONLY | ABL_NO_LINES | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps));
+        put("b512_no_lookback", time_variant<512, ABL_NO_LOOKBACK>(c, 1, reps));
+        put("b512_no_lines", time_variant<512, ABL_NO_LINES>(c, 1, reps));
+        put("b512_no_prologue", time_variant<512, ABL_NO_PROLOGUE>(c, 1, reps));
+        put("b512_load_only", time_variant<512, ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps));
+        put("b512_no_lines_s4", time_variant<512, ABL_NO_LINES>(c, 4, reps));
+        put("b512_load_only_s4", time_variant<512, ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 4, reps));
         put("read_kernel_s1", time_variant<256, 0xFFFFu>(c, 1, reps));
         put("read_kernel_s4", time_variant<256, 0xFFFFu>(c, 4, reps));
     }
@@ -164,10 +164,10 @@ int main(int argc, char **argv) {
         CK(hipMemcpyAsync(&n, c.d_n, 8, hipMemcpyDeviceToHost, c.s[0]));
         CK(hipStreamSynchronize(c.s[0]));
         fprintf(stderr, "b1024 lines %llu expected %zu\n", (unsigned long long)n, lines[0]);
-        launch_route<256, ABL_NONE>(c.ds[0], p, c.s[0]);
+        launch_route<512, ABL_NONE>(c.ds[0], p, c.s[0]);
         CK(hipMemcpyAsync(&n, c.d_n, 8, hipMemcpyDeviceToHost, c.s[0]));
         CK(hipStreamSynchronize(c.s[0]));
-        fprintf(stderr, "b256 lines %llu expected %zu\n", (unsigned long long)n, lines[0]);
+        fprintf(stderr, "b512 lines %llu expected %zu\n", (unsigned long long)n, lines[0]);
     }
     printf("{\"line_len\": %u, \"batch_bytes\": %zu, \"us_per_batch\": {", line_len, batch);
     for (size_t r = 0; r < rows.size(); ++r) {

@@ -1,0 +1,112 @@
+// Diagnostic timeline of route_kernel (ABL_STAMPS build): s_memrealtime (100 MHz) at phase
+// boundaries in every workgroup, for back-to-back launches on 16 distinct batches.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/stamps_route tools/stamps_route.hip
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../statsd-router_amd/csrc/route_host.hpp"
+
+extern "C" {
+#include "../statsd-router_amd/csrc/sr_gen.c"
+}
+
+using namespace srk;
+
+#define CK(x)                                                                         \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                                  \
+        }                                                                             \
+    } while (0)
+
+static double med(std::vector<double> v) {
+    if (v.empty()) return 0;
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+}
+
+template <int BLOCK>
+void run(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size_t> &sizes, sr_record *d_out,
+         size_t max_lines, uint64_t *d_n, uint64_t *d_dbg, hipStream_t s, uint32_t line_len) {
+    const int L = (int)batches.size();
+    const uint32_t T = BLOCK * kLaneBytes;
+    const uint32_t ntiles = (uint32_t)((sizes[0] + T - 1) / T);
+    std::vector<uint64_t> h((size_t)L * ntiles * 8);
+    for (int w = 0; w < 4; ++w) {   // warm
+        RouteParams p = ds.params(batches[w], sizes[w], d_out, max_lines, nullptr, d_n);
+        p.dbg = d_dbg;
+        launch_route<BLOCK, ABL_STAMPS>(ds, p, s);
+    }
+    CK(hipStreamSynchronize(s));
+    for (int i = 0; i < L; ++i) {
+        RouteParams p = ds.params(batches[i], sizes[i], d_out, max_lines, nullptr, d_n);
+        p.dbg = d_dbg + (size_t)i * ntiles * 8;
+        launch_route<BLOCK, ABL_STAMPS>(ds, p, s);
+    }
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(h.data(), d_dbg, h.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<double> span, start_spread, end_spread, ph[6];
+    for (int i = 0; i < L; ++i) {
+        const uint64_t *d = h.data() + (size_t)i * ntiles * 8;
+        uint64_t s0 = ~0ull, s0max = 0, e0 = ~0ull, e1 = 0;
+        for (uint32_t b = 0; b < ntiles; ++b) {
+            s0 = std::min(s0, d[b * 8 + 0]);
+            s0max = std::max(s0max, d[b * 8 + 0]);
+            e0 = std::min(e0, d[b * 8 + 6]);
+            e1 = std::max(e1, d[b * 8 + 6]);
+            const double u = 0.01;   // us per tick
+            ph[0].push_back((d[b * 8 + 1] - d[b * 8 + 0]) * u);   // loads -> LDS
+            ph[1].push_back((d[b * 8 + 2] - d[b * 8 + 1]) * u);   // masks + scan
+            ph[2].push_back((d[b * 8 + 3] - d[b * 8 + 2]) * u);   // look-back (wave 0)
+            ph[3].push_back((d[b * 8 + 4] - d[b * 8 + 2]) * u);   // to staged lines
+            ph[4].push_back((d[b * 8 + 5] - d[b * 8 + 4]) * u);   // hash + records
+            ph[5].push_back((d[b * 8 + 6] - d[b * 8 + 0]) * u);   // workgroup lifetime
+        }
+        span.push_back((e1 - s0) * 0.01);
+        start_spread.push_back((s0max - s0) * 0.01);
+        end_spread.push_back((e1 - e0) * 0.01);
+    }
+    printf("{\"block\": %d, \"line_len\": %u, \"tiles\": %u, \"span_us\": %.2f, \"start_spread_us\": %.2f, "
+           "\"end_spread_us\": %.2f, \"median_us\": {\"load\": %.2f, \"masks_scan\": %.2f, \"lookback\": %.2f, "
+           "\"to_staged\": %.2f, \"hash_records\": %.2f, \"lifetime\": %.2f}}\n",
+           BLOCK, line_len, ntiles, med(span), med(start_spread), med(end_spread), med(ph[0]), med(ph[1]), med(ph[2]),
+           med(ph[3]), med(ph[4]), med(ph[5]));
+}
+
+int main(int argc, char **argv) {
+    const int L = 16;
+    const size_t batch = 16u << 20;
+    uint32_t line_len = argc > 1 ? (uint32_t)atoi(argv[1]) : 64;
+    CK(hipSetDevice(0));
+    DeviceState ds;
+    if (ds.init(batch, 4) != 0) return 1;
+    std::vector<uint8_t> host(batch);
+    std::vector<uint8_t *> batches;
+    std::vector<size_t> sizes;
+    size_t nl = 0, nd = 0;
+    for (int b = 0; b < L; ++b) {
+        const size_t n = sr_gen_stream(0x5EED0002ull + 65537ull * b, 0, &line_len, 1, 0.0, 4095, host.data(), batch,
+                                       nullptr, 0, &nd, &nl);
+        uint8_t *d;
+        CK(hipMalloc(&d, batch));
+        CK(hipMemcpy(d, host.data(), n, hipMemcpyHostToDevice));
+        batches.push_back(d);
+        sizes.push_back(n);
+    }
+    sr_record *d_out;
+    uint64_t *d_n, *d_dbg;
+    CK(hipMalloc(&d_out, nl * sizeof(sr_record)));
+    CK(hipMalloc(&d_n, 8));
+    CK(hipMalloc(&d_dbg, (size_t)L * 4096 * 8 * 8));
+    hipStream_t s;
+    CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    run<1024>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
+    run<512>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
+    run<256>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
+    return 0;
+}
