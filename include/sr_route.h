@@ -108,6 +108,22 @@ int sr_route_batch(sr_ctx *ctx, const uint8_t *bytes, size_t nbytes, sr_record *
 int sr_route_device(sr_ctx *ctx, const uint8_t *d_bytes, size_t nbytes, sr_record *d_out,
                     size_t max_records, uint64_t *d_hashes, uint64_t *d_n_records);
 
+/* Several device-resident batches in ONE launch (asynchronous, on the context's stream): the
+ * batches of several data threads (the reference's threads_num sockets, sr-main.c:237-308) are
+ * routed together, each exactly as sr_route_device would route it alone. Up to
+ * SR_MAX_BATCHES_PER_LAUNCH batches share a kernel launch; larger counts are split into several
+ * launches. Each batch must fit max_batch_bytes. Returns 0 or -EINVAL / -EIO. */
+#define SR_MAX_BATCHES_PER_LAUNCH 16u
+typedef struct sr_batch {
+    const uint8_t *d_bytes;  /* framed datagrams, device memory                         */
+    size_t nbytes;
+    sr_record *d_out;        /* max_records records, device memory                      */
+    size_t max_records;
+    uint64_t *d_hashes;      /* NULL or max_records u64, device memory                  */
+    uint64_t *d_n_records;   /* device u64: the batch's line count                      */
+} sr_batch;
+int sr_route_device_many(sr_ctx *ctx, const sr_batch *batches, size_t count);
+
 /* Wait for all work enqueued by this context. */
 int sr_sync(sr_ctx *ctx);
 

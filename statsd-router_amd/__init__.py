@@ -46,8 +46,17 @@ assert RECORD_DTYPE.itemsize == 8
 # every function the header declares (tests check the library exports exactly these)
 ABI_FUNCTIONS = (
     "sr_frame_datagram", "sr_frame_datagrams", "sr_open", "sr_set_alive", "sr_set_stream",
-    "sr_route_batch", "sr_route_device", "sr_sync", "sr_close", "sr_version",
+    "sr_route_batch", "sr_route_device", "sr_route_device_many", "sr_sync", "sr_close", "sr_version",
 )
+SR_MAX_BATCHES_PER_LAUNCH = 16
+
+
+class SrBatch(ctypes.Structure):
+    """struct sr_batch (include/sr_route.h): one device-resident batch of sr_route_device_many."""
+    _fields_ = [
+        ("d_bytes", ctypes.c_void_p), ("nbytes", ctypes.c_size_t), ("d_out", ctypes.c_void_p),
+        ("max_records", ctypes.c_size_t), ("d_hashes", ctypes.c_void_p), ("d_n_records", ctypes.c_void_p),
+    ]
 
 
 class SrError(OSError):
@@ -94,6 +103,7 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_set_stream": (ctypes.c_int, [vp, vp]),
         "sr_route_batch": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, c_size_p, vp]),
         "sr_route_device": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp, vp]),
+        "sr_route_device_many": (ctypes.c_int, [vp, ctypes.POINTER(SrBatch), ctypes.c_size_t]),
         "sr_sync": (ctypes.c_int, [vp]),
         "sr_close": (None, [vp]),
         "sr_version": (ctypes.c_char_p, []),
@@ -246,6 +256,13 @@ class Router:
         _check(self._lib.sr_route_device(self._h, ctypes.c_void_p(d_bytes), nbytes, ctypes.c_void_p(d_out),
                                          max_records, ctypes.c_void_p(d_hashes or 0), ctypes.c_void_p(d_count)),
                "sr_route_device")
+
+    def route_device_many(self, batches) -> None:
+        """sr_route_device_many: batches = [(d_bytes, nbytes, d_out, max_records, d_hashes, d_count), ...]."""
+        arr = (SrBatch * max(len(batches), 1))()
+        for i, (db, nb, do, mr, dh, dc) in enumerate(batches):
+            arr[i] = SrBatch(db, nb, do, mr, dh or None, dc)
+        _check(self._lib.sr_route_device_many(self._h, arr, len(batches)), "sr_route_device_many")
 
     def sync(self) -> None:
         _check(self._lib.sr_sync(self._h), "sr_sync")

@@ -62,7 +62,8 @@ struct DeviceState {
         max_batch = max_batch_bytes;
         nds = n_downstreams;
         nwords = (n_downstreams + 63) / 64;
-        max_tiles = (uint32_t)((max_batch_bytes + 16383) / 16384);   // enough for the smallest tile (256 threads)
+        // status granules for kMaxBatches batches of the smallest tile (256 threads, 16 KiB)
+        max_tiles = (uint32_t)(kMaxBatches * ((max_batch_bytes + 16383) / 16384));
         h_alive = (uint64_t *)calloc(nwords ? nwords : 1, sizeof(uint64_t));
         if (!h_alive) return -ENOMEM;
         if (hipMalloc(&d_alive, (nwords ? nwords : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
@@ -140,16 +141,10 @@ struct DeviceState {
         return hipStreamSynchronize(stream) == hipSuccess ? 0 : -EIO;
     }
 
-    RouteParams params(const uint8_t *d_bytes, size_t nbytes, sr_record *d_out, size_t max_records,
-                       uint64_t *d_hashes, uint64_t *d_n) const {
+    // launch parameters without batches (add them with add_batch)
+    RouteParams params() const {
         RouteParams p;
-        p.bytes = d_bytes;
-        p.nbytes = (uint32_t)nbytes;
-        p.ntiles = (uint32_t)(((uint64_t)nbytes + kTile - 1) / kTile);
-        p.recs = d_out;
-        p.hashes = d_hashes;
-        p.n_out = d_n;
-        p.max_records = (uint32_t)(max_records > 0xFFFFFFFFull ? 0xFFFFFFFFull : max_records);
+        memset(&p, 0, sizeof(p));
         p.nds = nds;
         p.dead = dead;
         p.pending_cap = pending_cap;
@@ -164,15 +159,67 @@ struct DeviceState {
         return p;
     }
 
+    // one-batch launch parameters
+    RouteParams params(const uint8_t *d_bytes, size_t nbytes, sr_record *d_out, size_t max_records,
+                       uint64_t *d_hashes, uint64_t *d_n) const {
+        RouteParams p = params();
+        add_batch(p, d_bytes, nbytes, d_out, max_records, d_hashes, d_n);
+        return p;
+    }
+
+    static bool add_batch(RouteParams &p, const uint8_t *d_bytes, size_t nbytes, sr_record *d_out,
+                          size_t max_records, uint64_t *d_hashes, uint64_t *d_n) {
+        if (p.nb >= (uint32_t)kMaxBatches) return false;
+        BatchDesc &b = p.b[p.nb++];
+        b.bytes = d_bytes;
+        b.nbytes = (uint32_t)nbytes;
+        b.recs = d_out;
+        b.hashes = d_hashes;
+        b.n_out = d_n;
+        b.max_records = (uint32_t)(max_records > 0xFFFFFFFFull ? 0xFFFFFFFFull : max_records);
+        b.tile0 = b.ntiles = 0;
+        return true;
+    }
+
     bool wide() const { return dead > (uint32_t)kOverlay && dead < nds; }
 };
 
+// Launch the route kernel over the batches of p (tile ranges assigned here; empty batches get a
+// zero line count without a kernel). With more than kOverlay dead shards every batch is launched
+// on its own so that the deferred-probe list holds one batch at a time.
 template <int BLOCK, unsigned ABL>
-inline int launch_route(const DeviceState &ds, RouteParams p, hipStream_t stream) {
-    constexpr uint32_t T = BLOCK * kLaneBytes;
-    p.ntiles = (uint32_t)(((uint64_t)p.nbytes + T - 1) / T);
+inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_t stream) {
+    constexpr uint64_t T = (uint64_t)BLOCK * kLaneBytes;
+    if (ds.wide() && in.nb > 1) {
+        for (uint32_t i = 0; i < in.nb; ++i) {
+            RouteParams one = in;
+            one.nb = 1;
+            one.b[0] = in.b[i];
+            const int rc = launch_route<BLOCK, ABL>(ds, one, stream);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    RouteParams p = in;
+    p.nb = 0;
+    uint32_t tiles = 0;
+    for (uint32_t i = 0; i < in.nb; ++i) {
+        const BatchDesc &b = in.b[i];
+        if (b.nbytes == 0) {
+            if (hipMemsetAsync(b.n_out, 0, sizeof(uint64_t), stream) != hipSuccess) return -EIO;
+            continue;
+        }
+        BatchDesc &d = p.b[p.nb++];
+        d = b;
+        d.tile0 = tiles;
+        d.ntiles = (uint32_t)((b.nbytes + T - 1) / T);
+        tiles += d.ntiles;
+    }
+    if (tiles == 0) return 0;
+    if (tiles > ds.max_tiles) return -EINVAL;
+    p.total_tiles = tiles;
     if (ds.wide() && hipMemsetAsync(&ds.d_ctl->pending, 0, sizeof(uint32_t), stream) != hipSuccess) return -EIO;
-    hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.ntiles), dim3(BLOCK), 0, stream, p);
+    hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(tiles), dim3(BLOCK), 0, stream, p);
     if (hipGetLastError() != hipSuccess) return -EIO;
     if (ds.wide()) {
         static bool attr_set = false;

@@ -46,9 +46,9 @@
 
 namespace srk {
 
-constexpr int kBlock = 1024;                 // threads per workgroup of the product kernel (16 waves)
+constexpr int kBlock = 512;                  // threads per workgroup of the product kernel (8 waves)
 constexpr int kLaneBytes = 64;               // bytes per lane
-constexpr int kTile = kBlock * kLaneBytes;   // 64 KiB per tile
+constexpr int kTile = kBlock * kLaneBytes;   // 32 KiB per tile
 constexpr int kOverlay = 16;                 // register overlay entries of the probe
 constexpr int kNone = 0x1FFFF;               // "no colon" marker (above any tile position)
 constexpr int kSpinBudget = 1 << 14;         // polls before a missing predecessor is proxied
@@ -98,7 +98,7 @@ struct Magic {          // exact n / d for 64-bit n (Granlund-Montgomery, round-
 
 struct PendingLine {
     uint32_t rec;
-    uint32_t pad;
+    uint32_t batch;
     uint64_t hash;
 };
 
@@ -111,14 +111,24 @@ struct Control {
     uint32_t done[8][32];
 };
 
-struct RouteParams {
+// One batch of a launch. A launch routes up to kMaxBatches independent batches: tiles
+// [tile0, tile0 + ntiles) of the grid belong to batch i, each batch with its own look-back chain
+// (status granules at the same grid indices) and its own records and line count.
+constexpr int kMaxBatches = 16;
+struct BatchDesc {
     const uint8_t *bytes;
-    uint32_t nbytes;
-    uint32_t ntiles;
     sr_record *recs;
     uint64_t *hashes;        // may be null
-    uint64_t *n_out;         // device: total line count
+    uint64_t *n_out;         // device: line count of the batch
+    uint32_t nbytes;
     uint32_t max_records;
+    uint32_t tile0;
+    uint32_t ntiles;
+};
+
+struct RouteParams {
+    uint32_t nb;             // batches in this launch
+    uint32_t total_tiles;    // grid size
     uint32_t nds;            // number of downstreams
     uint32_t dead;           // dead downstreams in the alive snapshot
     uint32_t pending_cap;
@@ -130,6 +140,7 @@ struct RouteParams {
     uint64_t *status;        // per-tile look-back granules
     PendingLine *pending;
     uint64_t *dbg;           // ABL_STAMPS builds only: 8 timestamps per tile
+    BatchDesc b[kMaxBatches];
 };
 
 // ---------------------------------------------------------------------------------------
@@ -432,11 +443,11 @@ __device__ __forceinline__ uint4 img_get16(const S &sm, int b) {
 // Number of '\n' bytes in tile m, counted by one wave (only used when a predecessor has not
 // published its count within the spin budget).
 template <int BLOCK>
-__device__ uint32_t count_tile_wave(const RouteParams &p, __amdgpu_buffer_rsrc_t rsrc, uint32_t m, int lane) {
+__device__ uint32_t count_tile_wave(uint32_t nbytes, __amdgpu_buffer_rsrc_t rsrc, uint32_t m, int lane) {
     constexpr uint32_t T = BLOCK * kLaneBytes;
     uint32_t c = 0;
     for (uint32_t off = lane * 16; off < T; off += 1024) {
-        const uint4 v = load16(rsrc, m * T + off, p.nbytes);
+        const uint4 v = load16(rsrc, m * T + off, nbytes);
         c += eq_count4(v.x, 0x0A0A0A0Au) + eq_count4(v.y, 0x0A0A0A0Au) + eq_count4(v.z, 0x0A0A0A0Au) +
              eq_count4(v.w, 0x0A0A0A0Au);
     }
@@ -448,18 +459,18 @@ __device__ uint32_t count_tile_wave(const RouteParams &p, __amdgpu_buffer_rsrc_t
 constexpr int kLookPer = 4;   // predecessors per lane per look-back round
 
 // First round of status loads, issued early so their latency hides behind the mask pass.
-__device__ __forceinline__ void look_back_prefetch(const RouteParams &p, uint32_t t, int lane,
+__device__ __forceinline__ void look_back_prefetch(const uint64_t *status, uint32_t t, int lane,
                                                    uint64_t (&first)[kLookPer]) {
 #pragma unroll
     for (int k = 0; k < kLookPer; ++k) {
         const int64_t idx = (int64_t)t - 1 - lane - 64 * k;
-        first[k] = idx >= 0 ? __hip_atomic_load(&p.status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        first[k] = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     }
 }
 
 template <int BLOCK>
-__device__ uint32_t look_back_wave(const RouteParams &p, __amdgpu_buffer_rsrc_t rsrc, uint32_t t, uint32_t epoch,
-                                   int lane, const uint64_t (&first)[kLookPer]) {
+__device__ uint32_t look_back_wave(const uint64_t *status, uint32_t nbytes, __amdgpu_buffer_rsrc_t rsrc, uint32_t t,
+                                   uint32_t epoch, int lane, const uint64_t (&first)[kLookPer]) {
     constexpr int kPer = kLookPer;
     uint64_t acc = 0;
     int64_t hi = t;
@@ -482,7 +493,7 @@ __device__ uint32_t look_back_wave(const RouteParams &p, __amdgpu_buffer_rsrc_t 
 #pragma unroll
             for (int k = 0; k < kPer; ++k) {
                 if (!need[k]) continue;
-                st[k] = __hip_atomic_load(&p.status[hi - 1 - lane - 64 * k], __ATOMIC_RELAXED,
+                st[k] = __hip_atomic_load(&status[hi - 1 - lane - 64 * k], __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
                 need[k] = !((uint32_t)(st[k] >> 34) == ep && ((st[k] >> 32) & 3u) != 0);
                 pending |= need[k];
@@ -501,7 +512,7 @@ __device__ uint32_t look_back_wave(const RouteParams &p, __amdgpu_buffer_rsrc_t 
                 const int L = __builtin_ctzll(mask);
                 mask &= mask - 1;
                 const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(hi - 1 - L - 64 * k), L);
-                const uint32_t cnt = count_tile_wave<BLOCK>(p, rsrc, m, lane);
+                const uint32_t cnt = count_tile_wave<BLOCK>(nbytes, rsrc, m, lane);
                 if (lane == L) {
                     st[k] = mk_status(epoch, kFlagAgg, cnt);
                     need[k] = false;
@@ -547,12 +558,21 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const uint32_t t = blockIdx.x;
+    const uint32_t g = blockIdx.x;
+    // the batch of this tile (uniform; at most kMaxBatches scalar compares)
+    uint32_t bi = 0;
+    for (uint32_t k = 1; k < p.nb; ++k)
+        if (g >= p.b[k].tile0) bi = k;
+    const BatchDesc &bd = p.b[bi];
+    const uint8_t *const bytes = bd.bytes;
+    const uint32_t nbytes = bd.nbytes, ntiles = bd.ntiles;
+    uint64_t *const status = p.status + bd.tile0;
+    const uint32_t t = g - bd.tile0;   // tile index within the batch
     const int64_t T0 = (int64_t)t * kTileB;
     const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)p.bytes, (short)0, (int)p.nbytes, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)bytes, (short)0, (int)nbytes, 0x00020000);
 
-    stamp<ABL>(p, tid, t, 0);
+    stamp<ABL>(p, tid, g, 0);
     if (tid == 0) sm.epoch = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < kPowTable) (&sm.kp_lo[0])[tid] = p.kpow[tid];   // kp_lo | kp_hi | kinv are contiguous
     if (tid < kHalo / 16) {   // the 2 KiB before the tile (zeros before the batch start)
@@ -568,7 +588,7 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
         uint4 v[4];
         uint32_t cnt = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = load16(rsrc, (uint32_t)T0 + k * BLOCK * 16 + tid * 16, p.nbytes);
+        for (int k = 0; k < 4; ++k) v[k] = load16(rsrc, (uint32_t)T0 + k * BLOCK * 16 + tid * 16, nbytes);
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             img_put16(sm, kHalo + 16 * (k * BLOCK + tid), v[k]);
@@ -579,19 +599,19 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
         if (lane == 0) sm.wave_cnt[wave] = cnt;
     }
     __syncthreads();
-    stamp<ABL>(p, tid, t, 1);
+    stamp<ABL>(p, tid, g, 1);
     const uint32_t epoch = sm.epoch;
     uint32_t tile_count = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) tile_count += sm.wave_cnt[w];
     if (tid == 0) {   // publish this tile's aggregate (tile 0: its inclusive prefix)
         const uint64_t st = mk_status(epoch, t == 0 ? kFlagIncl : kFlagAgg, tile_count);
-        __hip_atomic_store(&p.status[t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&status[t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     uint64_t lb_first[kLookPer] = {0ull, 0ull, 0ull, 0ull};
-    if (wave == 0 && !(ABL & ABL_NO_LOOKBACK)) look_back_prefetch(p, t, lane, lb_first);
+    if (wave == 0 && !(ABL & ABL_NO_LOOKBACK)) look_back_prefetch(status, t, lane, lb_first);
     if (ABL & ABL_LOAD_ONLY) {
-        if (tid == 0 && t == p.ntiles - 1) *p.n_out = tile_count;
+        if (tid == 0 && t == ntiles - 1) *bd.n_out = tile_count;
         __syncthreads();
     } else {
     // ---- per lane: '\n' / ':' masks of its 64 contiguous bytes, segmented line-state scan -------
@@ -622,7 +642,7 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
     const uint64_t sseg = wave_scan64(seg, (uint64_t)kNone, comb);
     if (lane == 63) sm.wave_seg[wave] = sseg;
     __syncthreads();
-    stamp<ABL>(p, tid, t, 2);
+    stamp<ABL>(p, tid, g, 2);
     if (wave == 0) {   // exclusive line state of every wave
         const uint64_t v = wave_scan64(lane < kWaves ? sm.wave_seg[lane] : (uint64_t)kNone, (uint64_t)kNone, comb);
         const uint64_t ex = wave_shr1_64(v, (uint64_t)kNone);
@@ -636,17 +656,17 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
     if (wave == 0) {
         uint32_t base = 0;
         if (!(ABL & ABL_NO_LOOKBACK)) {
-            base = look_back_wave<BLOCK>(p, rsrc, t, epoch, lane, lb_first);
+            base = look_back_wave<BLOCK>(status, nbytes, rsrc, t, epoch, lane, lb_first);
             if (lane == 0 && t > 0) {
                 const uint64_t st = mk_status(epoch, kFlagIncl, base + tile_count);
-                __hip_atomic_store(&p.status[t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&status[t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         if (lane == 0) {
             sm.base = base;
-            if (t == p.ntiles - 1) *p.n_out = (uint64_t)base + tile_count;
+            if (t == ntiles - 1) *bd.n_out = (uint64_t)base + tile_count;
         }
-        stamp<ABL>(p, tid, t, 3);
+        stamp<ABL>(p, tid, g, 3);
     }
     // ---- last wave: where the line that straddles into the tile starts, its first ':' ----------
     if (wave == kPreWave) {
@@ -670,7 +690,7 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
                     const int64_t lo = hi - 1024 > 0 ? hi - 1024 : 0;
                     a = lo + lane * 16;
                     nl16 = 0;
-                    if (a < hi) nl16 = eq_mask16(load16(rsrc, (uint32_t)a, p.nbytes), 0x0A0A0A0Au);
+                    if (a < hi) nl16 = eq_mask16(load16(rsrc, (uint32_t)a, nbytes), 0x0A0A0A0Au);
                     mm = __ballot(nl16 != 0);
                     hi = lo;
                 }
@@ -729,7 +749,7 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
             }
         }
         __syncthreads();
-        if (wbase == 0) stamp<ABL>(p, tid, t, 4);
+        if (wbase == 0) stamp<ABL>(p, tid, g, 4);
         if (!(ABL & ABL_NO_LINES)) {
             const uint32_t base = sm.base;
             const int s_pre = sm.s_pre;
@@ -765,41 +785,41 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
                     else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
                     else route = probe_shard(h, p);                                                    // :145
                     const uint32_t rec = base + (uint32_t)j;
-                    if (rec < p.max_records) {
+                    if (rec < bd.max_records) {
                         if (route == kRoutePending) {
                             const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
-                            if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, 0u, h};
+                            if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
                         }
                         sr_record r;
                         r.offset = (uint32_t)(T0 + s);
                         r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
                         r.route = (uint16_t)route;
-                        p.recs[rec] = r;
-                        if (p.hashes) p.hashes[rec] = h;
+                        bd.recs[rec] = r;
+                        if (bd.hashes) bd.hashes[rec] = h;
                     }
                 }
             }
         }
         __syncthreads();
-        if (wbase == 0) stamp<ABL>(p, tid, t, 5);
+        if (wbase == 0) stamp<ABL>(p, tid, g, 5);
         if (tid == 0) sm.lend[0] = sm.lend[min(kWin, (int)tile_count - wbase)];
         __syncthreads();
     }
     }
-    stamp<ABL>(p, tid, t, 6);
+    stamp<ABL>(p, tid, g, 6);
 
     // ---- arrivals: every workgroup adds itself (no return value, nothing waits); the last tile
     // waits until all have arrived, then resets the counters and advances the epoch. Every
     // workgroup read the epoch before arriving, so none of this launch can see the new one.
     if (tid == 0) {
-        __hip_atomic_fetch_add(&p.ctl->done[t & 7u][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (t == p.ntiles - 1) {
+        __hip_atomic_fetch_add(&p.ctl->done[g & 7u][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (g == p.total_tiles - 1) {
             for (uint32_t spin = 0; spin < (1u << 26); ++spin) {
                 uint32_t n = 0;
 #pragma unroll
                 for (int s8 = 0; s8 < 8; ++s8)
                     n += __hip_atomic_load(&p.ctl->done[s8][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (n >= p.ntiles) break;
+                if (n >= p.total_tiles) break;
                 __builtin_amdgcn_s_sleep(2);
             }
 #pragma unroll
@@ -836,7 +856,7 @@ __global__ __launch_bounds__(64) void probe_wide_kernel(RouteParams p) {
             }
             h = (h * 7 + 5) / 3;
         }
-        p.recs[pl.rec].route = (uint16_t)route;
+        p.b[pl.batch].recs[pl.rec].route = (uint16_t)route;
         // restore the identity on every touched position
         h = pl.hash;
         for (uint32_t i = n; i > 0 && steps > 0; --i, --steps) {

@@ -57,7 +57,7 @@ size_t sr_frame_datagrams(uint8_t *dst, size_t dst_cap, const uint8_t *const *dg
 }
 
 const char *sr_version(void) {
-    return "statsd-router-mi355x 0.3 (gfx950 route_kernel: 64 KiB tiles x 1024 threads, one-wave look-back)";
+    return "statsd-router-mi355x 0.4 (gfx950 route_kernel: 32 KiB tiles x 512 threads, up to 16 batches per launch)";
 }
 
 void sr_close(sr_ctx *c) {
@@ -122,10 +122,28 @@ int sr_route_device(sr_ctx *c, const uint8_t *d_bytes, size_t nbytes, sr_record 
     if (!c || !d_n_records || (nbytes && !d_bytes) || nbytes > c->ds.max_batch) return -EINVAL;
     if (max_records && !d_out) return -EINVAL;
     (void)hipSetDevice(c->device);
-    if (nbytes == 0)
-        return hipMemsetAsync(d_n_records, 0, sizeof(uint64_t), c->stream) == hipSuccess ? 0 : -EIO;
     const RouteParams p = c->ds.params(d_bytes, nbytes, d_out, max_records, d_hashes, d_n_records);
     return launch_route<kBlock, ABL_NONE>(c->ds, p, c->stream);
+}
+
+int sr_route_device_many(sr_ctx *c, const sr_batch *batches, size_t count) {
+    static_assert(SR_MAX_BATCHES_PER_LAUNCH == (unsigned)kMaxBatches, "launch batch limit");
+    if (!c || (count && !batches)) return -EINVAL;
+    for (size_t i = 0; i < count; ++i) {
+        const sr_batch &b = batches[i];
+        if (!b.d_n_records || (b.nbytes && !b.d_bytes) || b.nbytes > c->ds.max_batch) return -EINVAL;
+        if (b.max_records && !b.d_out) return -EINVAL;
+    }
+    (void)hipSetDevice(c->device);
+    for (size_t i0 = 0; i0 < count; i0 += kMaxBatches) {
+        RouteParams p = c->ds.params();
+        for (size_t i = i0; i < count && i < i0 + kMaxBatches; ++i)
+            DeviceState::add_batch(p, batches[i].d_bytes, batches[i].nbytes, batches[i].d_out, batches[i].max_records,
+                                   batches[i].d_hashes, batches[i].d_n_records);
+        const int rc = launch_route<kBlock, ABL_NONE>(c->ds, p, c->stream);
+        if (rc) return rc;
+    }
+    return 0;
 }
 
 int sr_route_batch(sr_ctx *c, const uint8_t *bytes, size_t nbytes, sr_record *out, size_t max_records,

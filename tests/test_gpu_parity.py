@@ -206,3 +206,44 @@ def test_device_resident_path(pkg, oracle):
         recs = d_out.cpu().numpy().view(pkg.RECORD_DTYPE)
         hs = d_h.cpu().numpy().view(np.uint64)
         _assert_same((recs, hs, int(d_n.item())), oracle.route(s.data, 4), "device path")
+
+
+@pytest.mark.parametrize("dead", [0, 1, 20])
+def test_device_many_batches_one_launch(pkg, oracle, dead):
+    """sr_route_device_many: batches of different shapes (incl. empty and tiny ones) routed in one
+    launch, each exactly as the oracle routes it alone; 20 dead of 40 takes the wide probe path
+    (one launch per batch)."""
+    import torch
+
+    n = 40
+    alive = [0 if k < dead else 1 for k in range(n)]
+    parts = [
+        pkg.gen_stream(3 << 20, [64], seed=11).data,
+        np.frombuffer(b"", dtype=np.uint8),
+        np.frombuffer(pkg.frame_datagrams(_hostile_stream(5, 200_000)), dtype=np.uint8),
+        np.frombuffer(b"a:1|c\n", dtype=np.uint8),
+        pkg.gen_stream(1 << 20, [256], seed=12, p_invalid=0.1).data,
+        np.frombuffer(_lines_stream([1449, 7, 1, 1600, 64] * 300, seed=3), dtype=np.uint8),
+    ] + [pkg.gen_stream(70_000 + 9_999 * i, [64, 256, 1024], seed=20 + i).data for i in range(14)]
+    with pkg.Router(n, 4 << 20) as r:
+        r.set_alive(alive)
+        stream = torch.cuda.current_stream()
+        r.set_stream(stream.cuda_stream)
+        d_in, d_out, d_h, descs = [], [], [], []
+        d_n = torch.full((len(parts),), -1, dtype=torch.int64, device="cuda")
+        for i, p in enumerate(parts):
+            cap = max(int(p.size), 1)
+            d_in.append(torch.from_numpy(p.copy() if p.size else np.zeros(1, np.uint8)).to("cuda"))
+            d_out.append(torch.empty(cap * 8, dtype=torch.uint8, device="cuda"))
+            d_h.append(torch.empty(cap, dtype=torch.int64, device="cuda"))
+            descs.append((d_in[-1].data_ptr(), int(p.size), d_out[-1].data_ptr(), cap, d_h[-1].data_ptr(),
+                          d_n.data_ptr() + 8 * i))
+        for _ in range(2):
+            r.route_device_many(descs)
+        torch.cuda.synchronize()
+        counts = d_n.cpu().numpy()
+        for i, p in enumerate(parts):
+            k = int(counts[i])
+            recs = d_out[i].cpu().numpy().view(pkg.RECORD_DTYPE)[:k]
+            hs = d_h[i].cpu().numpy().view(np.uint64)[:k]
+            _assert_same((recs, hs, k), oracle.route(p, n, alive), f"batch {i}")

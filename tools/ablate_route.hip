@@ -54,17 +54,22 @@ struct Ctx {
     hipEvent_t fork, join[kMaxS];
 };
 
+// S streams, M batches per launch (launch i routes batches i*M .. i*M+M-1 on stream i % S)
 template <int BLOCK, unsigned V>
-float time_variant(Ctx &c, int S, int reps) {
+float time_variant(Ctx &c, int S, int reps, int M = 1) {
     const int B = (int)c.batches.size();
     auto launch = [&](int i) {
-        const int k = i % B, st = i % S;
+        const int st = i % S;
         if (V == 0xFFFFu) {
+            const int k = i % B;
             hipLaunchKernelGGL(read_kernel, dim3((c.sizes[k] + 16383) / 16384), dim3(256), 0, c.s[st], c.batches[k],
                                (uint32_t)c.sizes[k], c.sink);
         } else {
-            const RouteParams p =
-                c.ds[st].params(c.batches[k], c.sizes[k], c.d_out[st], c.max_lines, nullptr, c.d_n + k);
+            RouteParams p = c.ds[st].params();
+            for (int m = 0; m < M; ++m) {
+                const int k = (i * M + m) % B;
+                DeviceState::add_batch(p, c.batches[k], c.sizes[k], c.d_out[st], c.max_lines, nullptr, c.d_n + k);
+            }
             launch_route<BLOCK, V>(c.ds[st], p, c.s[st]);
         }
     };
@@ -73,7 +78,8 @@ float time_variant(Ctx &c, int S, int reps) {
     CK(hipStreamBeginCapture(c.s[0], hipStreamCaptureModeGlobal));
     CK(hipEventRecord(c.fork, c.s[0]));
     for (int st = 1; st < S; ++st) CK(hipStreamWaitEvent(c.s[st], c.fork, 0));
-    for (int i = 0; i < B; ++i) launch(i);
+    const int nl = V == 0xFFFFu ? B : B / M;
+    for (int i = 0; i < nl; ++i) launch(i);
     for (int st = 1; st < S; ++st) {
         CK(hipEventRecord(c.join[st], c.s[st]));
         CK(hipStreamWaitEvent(c.s[0], c.join[st], 0));
@@ -141,6 +147,18 @@ int main(int argc, char **argv) {
             rows[i++].us[round] = us;
         };
         put("b1024_full_s1", time_variant<1024, ABL_NONE>(c, 1, reps));
+        put("b1024_m2", time_variant<1024, ABL_NONE>(c, 1, reps, 2));
+        put("b1024_m4", time_variant<1024, ABL_NONE>(c, 1, reps, 4));
+        put("b1024_m8", time_variant<1024, ABL_NONE>(c, 1, reps, 8));
+        put("b1024_m16", time_variant<1024, ABL_NONE>(c, 1, reps, 16));
+        put("b512_m4", time_variant<512, ABL_NONE>(c, 1, reps, 4));
+        put("b512_m8", time_variant<512, ABL_NONE>(c, 1, reps, 8));
+        put("b512_m16", time_variant<512, ABL_NONE>(c, 1, reps, 16));
+        put("b256_m8", time_variant<256, ABL_NONE>(c, 1, reps, 8));
+        put("b256_m16", time_variant<256, ABL_NONE>(c, 1, reps, 16));
+        put("b512_m4_s4", time_variant<512, ABL_NONE>(c, 4, reps, 4));
+        put("b512_load_only_m8", time_variant<512, ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps, 8));
+        put("b1024_load_only_m8", time_variant<1024, ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps, 8));
         put("b512_full_s1", time_variant<512, ABL_NONE>(c, 1, reps));
         put("b256_full_s1", time_variant<256, ABL_NONE>(c, 1, reps));
         put("b1024_full_s2", time_variant<1024, ABL_NONE>(c, 2, reps));
@@ -168,6 +186,19 @@ int main(int argc, char **argv) {
         CK(hipMemcpyAsync(&n, c.d_n, 8, hipMemcpyDeviceToHost, c.s[0]));
         CK(hipStreamSynchronize(c.s[0]));
         fprintf(stderr, "b512 lines %llu expected %zu\n", (unsigned long long)n, lines[0]);
+    }
+    {   // multi-batch launch: every batch's line count
+        std::vector<uint64_t> n(16);
+        RouteParams p = c.ds[0].params();
+        for (int k = 0; k < 16; ++k)
+            DeviceState::add_batch(p, c.batches[k], c.sizes[k], c.d_out[0], c.max_lines, nullptr, c.d_n + k);
+        CK(hipMemsetAsync(c.d_n, 0xFF, 16 * 8, c.s[0]));
+        launch_route<512, ABL_NONE>(c.ds[0], p, c.s[0]);
+        CK(hipMemcpyAsync(n.data(), c.d_n, 16 * 8, hipMemcpyDeviceToHost, c.s[0]));
+        CK(hipStreamSynchronize(c.s[0]));
+        int bad = 0;
+        for (int k = 0; k < 16; ++k) bad += n[k] != lines[k];
+        fprintf(stderr, "b512 m16: %d of 16 batch counts wrong\n", bad);
     }
     printf("{\"line_len\": %u, \"batch_bytes\": %zu, \"us_per_batch\": {", line_len, batch);
     for (size_t r = 0; r < rows.size(); ++r) {
