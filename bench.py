@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=64)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batches", type=int, default=64, help="distinct batches in the rotating set")
+    ap.add_argument("--per-launch", type=int, default=16,
+                    help="batches routed per kernel launch (sr_route_device_many; 1 = sr_route_device)")
     ap.add_argument("--dead", type=float, default=0.0, help="fraction of dead downstreams")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu", action="store_true")
@@ -86,7 +88,9 @@ def main():
     for b, s in enumerate(host):
         d_in[b, : sizes[b]].copy_(torch.from_numpy(s.data))
     max_lines = max(lines)
-    d_out = torch.empty(max_lines * 8, dtype=torch.uint8, device=dev)
+    M = max(1, min(args.per_launch, pkg.SR_MAX_BATCHES_PER_LAUNCH, B))
+    # one record array per batch slot of a launch (batches of one launch never share records)
+    d_out = torch.empty((M, max_lines * 8), dtype=torch.uint8, device=dev)
     d_cnt = torch.zeros(B, dtype=torch.int64, device=dev)
     stream = torch.cuda.Stream(device=dev)
     router = pkg.Router(shards, batch_bytes, device=local)
@@ -94,25 +98,35 @@ def main():
     router.set_stream(stream.cuda_stream)
     in_ptr, out_ptr, cnt_ptr = d_in.data_ptr(), d_out.data_ptr(), d_cnt.data_ptr()
 
-    def launch(b):
-        router.route_device(in_ptr + b * batch_bytes, sizes[b], out_ptr, max_lines, None, cnt_ptr + 8 * b)
+    def launch_range(i0, i1):
+        """Steps i0 .. i1-1 (batch i % B each), M batches per kernel launch."""
+        for j0 in range(i0, i1, M):
+            descs = []
+            for m, i in enumerate(range(j0, min(j0 + M, i1))):
+                b = i % B
+                descs.append((in_ptr + b * batch_bytes, sizes[b], out_ptr + m * max_lines * 8, max_lines, None,
+                              cnt_ptr + 8 * b))
+            if M == 1:
+                router.route_device(*descs[0])
+            else:
+                router.route_device_many(descs)
+
+    def launch(i):   # one launch: steps i*M .. i*M+M-1
+        launch_range(i * M, i * M + M)
 
     with torch.cuda.stream(stream):
-        for i in range(max(args.warmup, 1)):
-            launch(i % B)
+        launch_range(0, max(args.warmup, 1))
         stream.synchronize()
         # capture the rotating set as one graph (+ a tail graph so exactly K steps are timed)
         K = args.steps
         g_full = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g_full, stream=stream):
-            for b in range(B):
-                launch(b)
+            launch_range(0, B)
         g_tail = None
         if K % B:
             g_tail = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g_tail, stream=stream):
-                for b in range(K % B):
-                    launch(b)
+                launch_range(0, K % B)
         g_full.replay()
         stream.synchronize()
 
@@ -135,14 +149,17 @@ def main():
         region_ms = ev0.elapsed_time(ev1)
 
         # per-launch durations (HIP events on the launch stream), outside the timed region
-        nprobe = min(K, 512)
+        nprobe = max(1, min(K, 512) // M)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nprobe)]
+        probe_bytes = 0
         for i, (a, z) in enumerate(evs):
             a.record(stream)
-            launch(i % B)
+            launch(i)
             z.record(stream)
+            probe_bytes += sum(sizes[j % B] for j in range(i * M, i * M + M))
         stream.synchronize()
         launch_ms = float(np.mean([a.elapsed_time(z) for a, z in evs]))
+        bytes_per_launch = probe_bytes / nprobe
 
     counts = d_cnt.cpu().numpy()
     assert all(int(counts[b]) == lines[b] for b in range(B)), "line counts differ from the generator"
@@ -160,7 +177,6 @@ def main():
 
     result = None
     if rank == 0:
-        bytes_per_launch = float(np.mean(sizes))
         achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
         traffic = None
         tj = args.traffic_json
@@ -191,7 +207,8 @@ def main():
                 "alive": f"{sum(alive)}/{shards}",
                 "rotating_batches": B,
                 "parallelism": f"dp{world} (independent datagram batches per GPU)",
-                "launch": "hipGraph replay of back-to-back route_kernel launches",
+                "batches_per_launch": M,
+                "launch": f"hipGraph replay of back-to-back route_kernel launches, {M} batches each",
             },
             "gib_per_s": round(total_bytes / wall_max / 2**30, 3),
             "gpu_region_ms": round(region_max * 1e3, 4),
@@ -205,7 +222,8 @@ def main():
                 "kernel": "route_kernel",
                 "bytes_per_launch": bytes_per_launch,
                 "launch_us": round(launch_ms * 1e3, 3),
-                "launch_timing": "mean of 512 eager launches, each bracketed by HIP events on its stream",
+                "launch_timing": f"mean of {nprobe} eager launches ({M} batches each), each bracketed by HIP events "
+                                 "on its stream",
             },
             "cpu_baseline": None,
         }
@@ -232,7 +250,7 @@ def main():
             }
 
         if not args.no_e2e:
-            result["e2e"] = e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev)
+            result["e2e"] = e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M)
     router.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -240,35 +258,58 @@ def main():
         dist.destroy_process_group()
 
 
-def e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, iters=64):
-    """Host memory -> H2D -> route -> D2H records, pinned buffers, one stream."""
-    nb = min(8, len(host))
+def e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M, groups=24):
+    """Host memory -> H2D -> route -> D2H records with pinned buffers ("end to end").
+
+    Groups of M batches, double-buffered: the H2D copy of group g+1 (copy stream) overlaps the
+    route launch of group g (the context's stream, M batches per launch as in the timed region)
+    and the D2H of group g-1's records (third stream)."""
+    nb = min(len(host), 2 * M)
     pinned = [torch.from_numpy(host[b].data).pin_memory() for b in range(nb)]
     max_lines = max(lines)
-    out_pinned = torch.empty(max_lines * 8, dtype=torch.uint8).pin_memory()
-    d_buf = torch.empty(batch_bytes, dtype=torch.uint8, device=dev)
-    d_out = torch.empty(max_lines * 8, dtype=torch.uint8, device=dev)
-    d_cnt = torch.zeros(1, dtype=torch.int64, device=dev)
-    with torch.cuda.stream(stream):
-        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        tot_lines = tot_bytes = 0
-        for it in range(iters + 4):
-            if it == 4:
-                stream.synchronize()
-                a.record(stream)
-                tot_lines = tot_bytes = 0
-            b = it % nb
-            d_buf[: sizes[b]].copy_(pinned[b], non_blocking=True)
-            router.route_device(d_buf.data_ptr(), sizes[b], d_out.data_ptr(), max_lines, None, d_cnt.data_ptr())
-            out_pinned[: lines[b] * 8].copy_(d_out[: lines[b] * 8], non_blocking=True)
-            tot_lines += lines[b]
-            tot_bytes += sizes[b]
-        z.record(stream)
-        stream.synchronize()
+    out_pinned = [torch.empty((M, max_lines * 8), dtype=torch.uint8).pin_memory() for _ in range(2)]
+    d_buf = [torch.empty((M, batch_bytes), dtype=torch.uint8, device=dev) for _ in range(2)]
+    d_out = [torch.empty((M, max_lines * 8), dtype=torch.uint8, device=dev) for _ in range(2)]
+    d_cnt = torch.zeros((2, M), dtype=torch.int64, device=dev)
+    h2d, d2h = torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)
+    ev_in = [torch.cuda.Event() for _ in range(2)]
+    ev_done = [torch.cuda.Event() for _ in range(2)]
+    ev_out = [torch.cuda.Event() for _ in range(2)]
+    a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    warm = 2
+    tot_lines = tot_bytes = 0
+    torch.cuda.synchronize()
+    for g in range(groups + warm):
+        if g == warm:
+            torch.cuda.synchronize()
+            a.record(h2d)
+            tot_lines = tot_bytes = 0
+        k = g % 2
+        bs = [(g * M + m) % nb for m in range(M)]
+        with torch.cuda.stream(h2d):
+            h2d.wait_event(ev_done[k])          # the route of group g-2 has consumed d_buf[k]
+            for m, b in enumerate(bs):
+                d_buf[k][m, : sizes[b]].copy_(pinned[b], non_blocking=True)
+            ev_in[k].record(h2d)
+        stream.wait_event(ev_in[k])
+        stream.wait_event(ev_out[k])            # group g-2's records have left d_out[k]
+        router.route_device_many([(d_buf[k][m].data_ptr(), sizes[b], d_out[k][m].data_ptr(), max_lines, None,
+                                   d_cnt[k, m].data_ptr()) for m, b in enumerate(bs)])
+        ev_done[k].record(stream)
+        with torch.cuda.stream(d2h):
+            d2h.wait_event(ev_done[k])
+            for m, b in enumerate(bs):
+                out_pinned[k][m, : lines[b] * 8].copy_(d_out[k][m, : lines[b] * 8], non_blocking=True)
+            ev_out[k].record(d2h)
+        tot_lines += sum(lines[b] for b in bs)
+        tot_bytes += sum(sizes[b] for b in bs)
+    z.record(d2h)
+    torch.cuda.synchronize()
     ms = a.elapsed_time(z)
     return {"value": round(tot_lines / (ms * 1e-3) / 1e6, 3), "unit": "M metrics/s",
             "gib_per_s": round(tot_bytes / (ms * 1e-3) / 2**30, 3),
-            "note": "pinned host batch -> H2D -> route_kernel -> D2H 8-B records, serial on one stream"}
+            "note": (f"pinned host batches -> H2D -> route_kernel ({M} batches per launch) -> D2H 8-B records; "
+                     "double-buffered on three streams (copy in / route / copy out)")}
 
 
 if __name__ == "__main__":
