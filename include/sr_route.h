@@ -124,6 +124,25 @@ typedef struct sr_batch {
 } sr_batch;
 int sr_route_device_many(sr_ctx *ctx, const sr_batch *batches, size_t count);
 
+/* ---- multi-GPU regroup ------------------------------------------------------ */
+/* Pack the VALID lines of a routed batch by owner GPU (owner of shard s = s % n_owners), ready for
+ * an all-to-all: for owner 0..n_owners-1 in turn, its lines in input order, each starting at a
+ * 4-byte aligned position (zero fill in between); d_out_recs gets one record per packed line in
+ * the same order, with `offset` relative to the start of its owner's chunk. d_owner_counts
+ * receives {lines, bytes} per owner (2*n_owners u64: the all-to-all split sizes). Lines routed
+ * to no shard are not packed (their WARN stays with the GPU that received them).
+ * d_recs / d_n_records: the output of sr_route_device for the same batch (same stream).
+ * out_cap >= SR_PACK_CAPACITY(nbytes) guarantees room; d_out_recs needs max_records entries.
+ * Asynchronous on the context's stream. n_owners in 1..64. Returns 0, -EINVAL, -ENOMEM, -EIO.
+ * The first call (or one with a larger max_records / n_owners) allocates scratch: not inside
+ * stream capture. */
+#define SR_MAX_OWNERS 64u
+#define SR_PACK_CAPACITY(nbytes) ((nbytes) + (nbytes) / 2u + 4u)
+int sr_pack_by_owner(sr_ctx *ctx, const uint8_t *d_bytes, size_t nbytes, const sr_record *d_recs,
+                     const uint64_t *d_n_records, size_t max_records, uint32_t n_owners,
+                     uint8_t *d_out_bytes, size_t out_cap, sr_record *d_out_recs,
+                     uint64_t *d_owner_counts);
+
 /* Wait for all work enqueued by this context. */
 int sr_sync(sr_ctx *ctx);
 

@@ -121,3 +121,35 @@ def run_reference(dgrams: Sequence[bytes], n_downstreams: int, alive=None) -> np
         hexw = ",".join(f"{int(x):x}" for x in w)
         subprocess.run([REF_HARNESS, str(n_downstreams), hexw, fin, fout], check=True)
         return np.fromfile(fout, dtype=REF_EVENT_DTYPE)
+
+
+def pack_by_owner(data, recs: np.ndarray, n_owners: int):
+    """Restatement of sr_pack_by_owner (include/sr_route.h), numpy, test-only.
+
+    Valid lines (route < 0xFFFD) grouped by owner = route % n_owners, input order within an owner;
+    each line starts at a 4-byte aligned position, zero fill in between. Returns
+    (packed bytes, packed records with offsets relative to the owner's chunk, counts[G, 2] =
+    {lines, bytes} per owner). Parity unpinned against the reference, which has no multi-GPU
+    path: what is pinned is the per-shard line sequence, compared with the oracle's routing."""
+    buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else np.asarray(data, np.uint8)
+    route = recs["route"].astype(np.int64)
+    valid = route < 0xFFFD
+    owner = np.where(valid, route % n_owners, -1)
+    idx = np.nonzero(valid)[0]
+    order = idx[np.argsort(owner[idx], kind="stable")]
+    lens = recs["length"][order].astype(np.int64)
+    len4 = (lens + 3) & ~3
+    pos = np.cumsum(len4) - len4                      # global position in the packed buffer
+    own = owner[order]
+    lines = np.bincount(own, minlength=n_owners).astype(np.int64)
+    nbytes = np.bincount(own, weights=len4, minlength=n_owners).astype(np.int64)
+    start = np.cumsum(nbytes) - nbytes
+    total = int(len4.sum())
+    out = np.zeros(total, dtype=np.uint8)
+    if lens.size:
+        seg = np.cumsum(lens) - lens
+        j = np.arange(int(lens.sum()), dtype=np.int64) - np.repeat(seg, lens)
+        out[np.repeat(pos, lens) + j] = buf[np.repeat(recs["offset"][order].astype(np.int64), lens) + j]
+    out_recs = recs[order].copy()
+    out_recs["offset"] = (pos - start[own]).astype(np.uint32)
+    return out, out_recs, np.stack([lines, nbytes], axis=1)

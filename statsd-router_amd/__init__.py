@@ -46,8 +46,15 @@ assert RECORD_DTYPE.itemsize == 8
 # every function the header declares (tests check the library exports exactly these)
 ABI_FUNCTIONS = (
     "sr_frame_datagram", "sr_frame_datagrams", "sr_open", "sr_set_alive", "sr_set_stream",
-    "sr_route_batch", "sr_route_device", "sr_route_device_many", "sr_sync", "sr_close", "sr_version",
+    "sr_route_batch", "sr_route_device", "sr_route_device_many", "sr_pack_by_owner", "sr_sync", "sr_close",
+    "sr_version",
 )
+SR_MAX_OWNERS = 64
+
+
+def pack_capacity(nbytes: int) -> int:
+    """SR_PACK_CAPACITY: packed-bytes room that always suffices for a batch of nbytes."""
+    return nbytes + nbytes // 2 + 4
 SR_MAX_BATCHES_PER_LAUNCH = 16
 
 
@@ -104,6 +111,8 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_route_batch": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, c_size_p, vp]),
         "sr_route_device": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp, vp]),
         "sr_route_device_many": (ctypes.c_int, [vp, ctypes.POINTER(SrBatch), ctypes.c_size_t]),
+        "sr_pack_by_owner": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, ctypes.c_uint32,
+                                            vp, ctypes.c_size_t, vp, vp]),
         "sr_sync": (ctypes.c_int, [vp]),
         "sr_close": (None, [vp]),
         "sr_version": (ctypes.c_char_p, []),
@@ -263,6 +272,14 @@ class Router:
         for i, (db, nb, do, mr, dh, dc) in enumerate(batches):
             arr[i] = SrBatch(db, nb, do, mr, dh or None, dc)
         _check(self._lib.sr_route_device_many(self._h, arr, len(batches)), "sr_route_device_many")
+
+    def pack_by_owner(self, d_bytes: int, nbytes: int, d_recs: int, d_n_records: int, max_records: int,
+                      n_owners: int, d_out_bytes: int, out_cap: int, d_out_recs: int, d_owner_counts: int) -> None:
+        """sr_pack_by_owner with raw device pointers (asynchronous on the context's stream)."""
+        vp = ctypes.c_void_p
+        _check(self._lib.sr_pack_by_owner(self._h, vp(d_bytes), nbytes, vp(d_recs), vp(d_n_records), max_records,
+                                          n_owners, vp(d_out_bytes), out_cap, vp(d_out_recs), vp(d_owner_counts)),
+               "sr_pack_by_owner")
 
     def sync(self) -> None:
         _check(self._lib.sr_sync(self._h), "sr_sync")

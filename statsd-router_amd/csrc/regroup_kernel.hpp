@@ -1,0 +1,234 @@
+// regroup_kernel.hpp — pack routed lines by owner GPU before the all-to-all regroup
+// (DESIGN.md §7).
+//
+// On a node of G GPUs every GPU routes its own datagram batches; shard s is then OWNED by GPU
+// s mod G, which sends it on to downstream s (the reference's push_to_downstream,
+// sr-main.c:73-83, runs on the owner). Before the exchange each GPU packs its valid lines by owner:
+//   out bytes : for owner 0, 1, ..., G-1 in turn, its lines in input order, each line starting at
+//               a 4-byte aligned position (zero fill after the line), so the copy is dword-wide;
+//   out recs  : one sr_record per packed line, same order; offset = position of the line
+//               relative to the start of its owner's chunk, length and route unchanged;
+//   counts    : per owner {lines, bytes} (u64 pairs) = the all-to-all split sizes.
+// Lines routed to no shard (invalid length / format, all dead) are not packed: the GPU that
+// received them reports them (the WARN lines of sr-main.c:115,142,184 stay with the receiver).
+//
+// Three launches over tiles of kPackTile records: per-tile counts, one workgroup scanning them,
+// then the stable scatter (in-tile ranks recomputed with ballots and DPP scans).
+#pragma once
+
+#include "route_kernel.hpp"
+
+namespace srk {
+
+constexpr int kPackBlock = 256;
+constexpr int kPackChunks = 8;                          // 256-record chunks per tile
+constexpr int kPackTile = kPackBlock * kPackChunks;     // records per tile
+constexpr int kMaxOwners = 64;
+
+struct PackParams {
+    const uint8_t *bytes;
+    uint32_t nbytes;
+    uint32_t n_owners;
+    const sr_record *recs;
+    const uint64_t *n_records;   // device line count written by the route kernel
+    uint32_t max_records;
+    uint32_t ntiles;
+    uint2 *tile_counts;          // [ntiles][n_owners] {lines, bytes} within the tile
+    uint2 *tile_base;            // [ntiles][n_owners] exclusive prefix over tiles within the owner
+    uint64_t *owner_start;       // [n_owners][2] {first line, first byte} of the owner's chunk
+    uint64_t *owner_counts;      // [n_owners][2] {lines, bytes} (output)
+    uint8_t *out_bytes;
+    uint64_t out_cap;
+    sr_record *out_recs;
+};
+
+__device__ __forceinline__ uint32_t pack_len4(uint32_t len) { return (len + 3u) & ~3u; }
+
+// inclusive wave scan of a u32 (DPP; no LDS)
+__device__ __forceinline__ uint32_t wave_incl_add32(uint32_t v) {
+    v += dpp32<kDppRowShr1>(0u, v);
+    v += dpp32<kDppRowShr2>(0u, v);
+    v += dpp32<kDppRowShr4>(0u, v);
+    v += dpp32<kDppRowShr8>(0u, v);
+    v += dpp32<kDppRowBcast15, 0xA>(0u, v);
+    v += dpp32<kDppRowBcast31, 0xC>(0u, v);
+    return v;
+}
+
+// owner of record r, or -1 when the line goes to no shard
+__device__ __forceinline__ int pack_owner(const sr_record &r, uint32_t n_owners) {
+    return r.route < SR_ROUTE_INVALID_LENGTH ? (int)(r.route % n_owners) : -1;
+}
+
+__global__ __launch_bounds__(kPackBlock) void pack_count_kernel(PackParams p) {
+    __shared__ uint32_t s_lines[kMaxOwners], s_bytes[kMaxOwners];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint32_t n = (uint32_t)min(*p.n_records, (uint64_t)p.max_records);
+    const uint32_t G = p.n_owners;
+    for (uint32_t o = tid; o < G; o += kPackBlock) s_lines[o] = s_bytes[o] = 0;
+    __syncthreads();
+    const uint32_t r0 = blockIdx.x * kPackTile;
+    for (int c = 0; c < kPackChunks; ++c) {
+        const uint32_t i = r0 + c * kPackBlock + tid;
+        int ow = -1;
+        uint32_t len4 = 0;
+        if (i < n) {
+            const sr_record r = p.recs[i];
+            ow = pack_owner(r, G);
+            len4 = pack_len4(r.length);
+        }
+        for (uint32_t o = 0; o < G; ++o) {
+            const uint64_t m = __ballot(ow == (int)o);
+            if (!m) continue;
+            const uint32_t b = wave_incl_add32(ow == (int)o ? len4 : 0u);
+            if (lane == 63) {
+                atomicAdd(&s_lines[o], (uint32_t)__popcll(m));
+                atomicAdd(&s_bytes[o], b);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t o = tid; o < G; o += kPackBlock)
+        p.tile_counts[(size_t)blockIdx.x * G + o] = make_uint2(s_lines[o], s_bytes[o]);
+}
+
+// one workgroup: per owner, exclusive scan of the tile counts; owner totals and chunk starts
+__global__ __launch_bounds__(1024) void pack_scan_kernel(PackParams p) {
+    __shared__ uint64_t s_tot[kMaxOwners][2];
+    __shared__ uint32_t s_carry[2];
+    __shared__ uint32_t s_wave[16][2];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t G = p.n_owners;
+    for (uint32_t o = 0; o < G; ++o) {
+        if (tid == 0) s_carry[0] = s_carry[1] = 0;
+        __syncthreads();
+        for (uint32_t t0 = 0; t0 < p.ntiles; t0 += 1024) {
+            const uint32_t t = t0 + tid;
+            const uint2 v = t < p.ntiles ? p.tile_counts[(size_t)t * G + o] : make_uint2(0, 0);
+            const uint32_t il = wave_incl_add32(v.x), ib = wave_incl_add32(v.y);
+            if (lane == 63) {
+                s_wave[wave][0] = il;
+                s_wave[wave][1] = ib;
+            }
+            __syncthreads();
+            uint32_t pl = s_carry[0], pb = s_carry[1];
+            for (int w = 0; w < wave; ++w) {
+                pl += s_wave[w][0];
+                pb += s_wave[w][1];
+            }
+            if (t < p.ntiles) p.tile_base[(size_t)t * G + o] = make_uint2(pl + il - v.x, pb + ib - v.y);
+            __syncthreads();
+            if (tid == 1023) {
+                s_carry[0] = pl + il;
+                s_carry[1] = pb + ib;
+            }
+            __syncthreads();
+        }
+        if (tid == 0) {
+            s_tot[o][0] = s_carry[0];
+            s_tot[o][1] = s_carry[1];
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        uint64_t line = 0, byte = 0;
+        for (uint32_t o = 0; o < G; ++o) {
+            p.owner_start[2 * o] = line;
+            p.owner_start[2 * o + 1] = byte;
+            p.owner_counts[2 * o] = s_tot[o][0];
+            p.owner_counts[2 * o + 1] = s_tot[o][1];
+            line += s_tot[o][0];
+            byte += s_tot[o][1];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) {
+    __shared__ uint32_t s_run_l[kMaxOwners], s_run_b[kMaxOwners];   // running in-tile position per owner
+    __shared__ uint32_t s_wl[4][kMaxOwners], s_wb[4][kMaxOwners];   // per-wave chunk totals
+    __shared__ uint32_t s_src[kPackBlock], s_dst[kPackBlock], s_len[kPackBlock];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t n = (uint32_t)min(*p.n_records, (uint64_t)p.max_records);
+    const uint32_t G = p.n_owners;
+    const uint32_t r0 = blockIdx.x * kPackTile;
+    for (uint32_t o = tid; o < G; o += kPackBlock) s_run_l[o] = s_run_b[o] = 0;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)p.bytes, (short)0, (int)p.nbytes, 0x00020000);
+    __syncthreads();
+    for (int c = 0; c < kPackChunks; ++c) {
+        const uint32_t i = r0 + c * kPackBlock + tid;
+        int ow = -1;
+        sr_record r{0, 0, 0};
+        if (i < n) {
+            r = p.recs[i];
+            ow = pack_owner(r, G);
+        }
+        const uint32_t len4 = pack_len4(r.length);
+        uint32_t my_l = 0, my_b = 0;   // exclusive rank / byte position among the wave's lines of my owner
+        for (uint32_t o = 0; o < G; ++o) {
+            const uint64_t m = __ballot(ow == (int)o);
+            if (!m) {
+                if (lane == 0) s_wl[wave][o] = s_wb[wave][o] = 0;
+                continue;
+            }
+            const uint32_t v = ow == (int)o ? len4 : 0u;
+            const uint32_t incl = wave_incl_add32(v);
+            if (ow == (int)o) {
+                my_l = __popcll(m & ((1ull << lane) - 1ull));
+                my_b = incl - v;
+            }
+            if (lane == 63) {
+                s_wl[wave][o] = (uint32_t)__popcll(m);
+                s_wb[wave][o] = incl;
+            }
+        }
+        __syncthreads();
+        uint32_t dst = 0;
+        if (ow >= 0) {
+            uint32_t pl = s_run_l[ow], pb = s_run_b[ow];
+            for (int w = 0; w < wave; ++w) {
+                pl += s_wl[w][ow];
+                pb += s_wb[w][ow];
+            }
+            const uint2 tb = p.tile_base[(size_t)blockIdx.x * G + ow];
+            const uint64_t line = p.owner_start[2 * ow] + tb.x + pl + my_l;
+            const uint32_t rel = tb.y + pb + my_b;   // byte position within the owner's chunk
+            dst = (uint32_t)(p.owner_start[2 * ow + 1] + rel);
+            sr_record o = r;
+            o.offset = rel;
+            p.out_recs[line] = o;
+        }
+        s_src[tid] = r.offset;
+        s_dst[tid] = dst;
+        s_len[tid] = ow >= 0 ? r.length : 0u;
+        __syncthreads();
+        if (tid < (int)G) {
+            uint32_t al = 0, ab = 0;
+            for (int w = 0; w < 4; ++w) {
+                al += s_wl[w][tid];
+                ab += s_wb[w][tid];
+            }
+            s_run_l[tid] += al;
+            s_run_b[tid] += ab;
+        }
+        // copy the chunk's lines: 16 lanes per line, one dword per lane per pass, 4-byte aligned
+        // destination, source realigned from two aligned dwords (buffer loads: no fault past the end)
+        const int sub = tid & 15;
+        for (int k = tid >> 4; k < kPackBlock; k += kPackBlock / 16) {
+            const uint32_t L = s_len[k];
+            if (L == 0) continue;
+            const uint32_t src = s_src[k], d = s_dst[k];
+            const uint32_t sh = src & 3u, sa = src & ~3u;
+            for (uint32_t q = 4u * sub; q < L; q += 64u) {
+                const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rsrc, sa + q, 0, 0);
+                const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rsrc, sa + q + 4u, 0, 0);
+                uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, sh);
+                if (q + 4u > L) v &= (1u << (8u * (L - q))) - 1u;   // zero fill after the line
+                if ((uint64_t)d + q + 4u <= p.out_cap) *(uint32_t *)(p.out_bytes + d + q) = v;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+}  // namespace srk

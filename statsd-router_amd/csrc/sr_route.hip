@@ -15,6 +15,7 @@
 #include <new>
 
 #include "../../include/sr_route.h"
+#include "regroup_kernel.hpp"
 #include "route_host.hpp"
 
 using namespace srk;
@@ -31,6 +32,10 @@ struct sr_ctx {
     uint64_t *d_hash;
     size_t d_hash_cap;
     uint64_t *d_count;
+    // scratch of sr_pack_by_owner
+    uint2 *d_pack_tiles;          // tile counts | tile bases
+    size_t pack_tiles_cap;        // entries per array
+    uint64_t *d_owner_start;
 };
 
 extern "C" {
@@ -69,6 +74,8 @@ void sr_close(sr_ctx *c) {
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_hash);
     (void)hipFree(c->d_count);
+    (void)hipFree(c->d_pack_tiles);
+    (void)hipFree(c->d_owner_start);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     free(c);
 }
@@ -142,6 +149,52 @@ int sr_route_device_many(sr_ctx *c, const sr_batch *batches, size_t count) {
                                    batches[i].d_hashes, batches[i].d_n_records);
         const int rc = launch_route<kBlock, ABL_NONE>(c->ds, p, c->stream);
         if (rc) return rc;
+    }
+    return 0;
+}
+
+int sr_pack_by_owner(sr_ctx *c, const uint8_t *d_bytes, size_t nbytes, const sr_record *d_recs,
+                     const uint64_t *d_n_records, size_t max_records, uint32_t n_owners, uint8_t *d_out_bytes,
+                     size_t out_cap, sr_record *d_out_recs, uint64_t *d_owner_counts) {
+    if (!c || !d_n_records || !d_owner_counts || n_owners == 0 || n_owners > SR_MAX_OWNERS) return -EINVAL;
+    if (nbytes > 0xFFFFFFF0ull || max_records > 0xFFFFFFFFull || out_cap > 0xFFFFFFFFull) return -EINVAL;
+    if (max_records && (!d_recs || !d_out_recs || !d_bytes || !d_out_bytes)) return -EINVAL;
+    (void)hipSetDevice(c->device);
+    const uint32_t ntiles = (uint32_t)((max_records + kPackTile - 1) / kPackTile);
+    const size_t need = (size_t)(ntiles ? ntiles : 1) * n_owners;
+    if (need > c->pack_tiles_cap) {
+        (void)hipFree(c->d_pack_tiles);
+        c->d_pack_tiles = nullptr;
+        c->pack_tiles_cap = 0;
+        if (hipMalloc(&c->d_pack_tiles, 2 * need * sizeof(uint2)) != hipSuccess) return -ENOMEM;
+        c->pack_tiles_cap = need;
+    }
+    if (!c->d_owner_start && hipMalloc(&c->d_owner_start, 2 * SR_MAX_OWNERS * sizeof(uint64_t)) != hipSuccess)
+        return -ENOMEM;
+    PackParams p;
+    p.bytes = d_bytes;
+    p.nbytes = (uint32_t)nbytes;
+    p.n_owners = n_owners;
+    p.recs = d_recs;
+    p.n_records = d_n_records;
+    p.max_records = (uint32_t)max_records;
+    p.ntiles = ntiles;
+    p.tile_counts = c->d_pack_tiles;
+    p.tile_base = c->d_pack_tiles + c->pack_tiles_cap;
+    p.owner_start = c->d_owner_start;
+    p.owner_counts = d_owner_counts;
+    p.out_bytes = d_out_bytes;
+    p.out_cap = out_cap;
+    p.out_recs = d_out_recs;
+    if (ntiles) {
+        hipLaunchKernelGGL(pack_count_kernel, dim3(ntiles), dim3(kPackBlock), 0, c->stream, p);
+        if (hipGetLastError() != hipSuccess) return -EIO;
+    }
+    hipLaunchKernelGGL(pack_scan_kernel, dim3(1), dim3(1024), 0, c->stream, p);
+    if (hipGetLastError() != hipSuccess) return -EIO;
+    if (ntiles) {
+        hipLaunchKernelGGL(pack_scatter_kernel, dim3(ntiles), dim3(kPackBlock), 0, c->stream, p);
+        if (hipGetLastError() != hipSuccess) return -EIO;
     }
     return 0;
 }

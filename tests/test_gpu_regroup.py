@@ -1,0 +1,75 @@
+"""GPU: sr_pack_by_owner (HIP) against the oracle's restatement, and the Regrouper end to end on a
+one-rank RCCL group (the multi-rank exchange is covered with gloo in test_regroup_dist.py)."""
+from __future__ import annotations
+
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _route_on_gpu(pkg, router, data, torch):
+    d_in = torch.from_numpy(np.ascontiguousarray(data) if data.size else np.zeros(1, np.uint8)).to("cuda")
+    cap = max(int(data.size), 1)
+    d_rec = torch.empty(cap, dtype=torch.int64, device="cuda")
+    d_n = torch.zeros(1, dtype=torch.int64, device="cuda")
+    router.route_device(d_in.data_ptr(), int(data.size), d_rec.data_ptr(), cap, None, d_n.data_ptr())
+    return d_in, d_rec, d_n, cap
+
+
+@pytest.mark.parametrize("G,n_shards,dead", [(1, 4, 0), (2, 64, 0), (3, 16, 2), (8, 64, 5), (64, 100, 0), (5, 3, 3)])
+def test_pack_by_owner_matches_oracle(pkg, oracle, G, n_shards, dead):
+    import torch
+
+    alive = [0 if k < dead else 1 for k in range(n_shards)]
+    data = pkg.gen_stream(3 << 20, [64, 256, 1024], seed=900 + G, p_invalid=0.1).data
+    with pkg.Router(n_shards, 4 << 20) as r:
+        r.set_alive(alive)
+        r.set_stream(torch.cuda.current_stream().cuda_stream)
+        d_in, d_rec, d_n, cap = _route_on_gpu(pkg, r, data, torch)
+        out_cap = pkg.pack_capacity(int(data.size))
+        d_pb = torch.full((out_cap,), 0xAB, dtype=torch.uint8, device="cuda")
+        d_pr = torch.empty(cap, dtype=torch.int64, device="cuda")
+        d_cnt = torch.empty((G, 2), dtype=torch.int64, device="cuda")
+        r.pack_by_owner(d_in.data_ptr(), int(data.size), d_rec.data_ptr(), d_n.data_ptr(), cap, G,
+                        d_pb.data_ptr(), out_cap, d_pr.data_ptr(), d_cnt.data_ptr())
+        torch.cuda.synchronize()
+        n = int(d_n.item())
+        recs = d_rec.cpu().numpy().view(pkg.RECORD_DTYPE)[:n]
+        eb, er, ec = oracle.pack_by_owner(data, recs, G)
+        cnt = d_cnt.cpu().numpy()
+        assert np.array_equal(cnt, ec), (cnt, ec)
+        tot_l, tot_b = int(ec[:, 0].sum()), int(ec[:, 1].sum())
+        got_r = d_pr.cpu().numpy().view(pkg.RECORD_DTYPE)[:tot_l]
+        assert np.array_equal(got_r, er)
+        got_b = d_pb.cpu().numpy()
+        assert np.array_equal(got_b[:tot_b], eb)
+        assert (got_b[tot_b:] == 0xAB).all()   # nothing written past the packed total
+
+
+def test_regrouper_one_rank_rccl(pkg, oracle):
+    import torch
+    import torch.distributed as dist
+
+    rg = importlib.import_module("statsd-router_amd.regroup")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    store = dist.TCPStore("127.0.0.1", 0, 1, True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1)
+    try:
+        data = pkg.gen_stream(2 << 20, [64, 256], seed=31, p_invalid=0.05).data
+        with pkg.Router(8, 4 << 20) as r:
+            r.set_stream(torch.cuda.current_stream().cuda_stream)
+            d_in, d_rec, d_n, cap = _route_on_gpu(pkg, r, data, torch)
+            reg = rg.Regrouper(pkg, r, 4 << 20, cap)
+            rb, rr, rc = reg(d_in.data_ptr(), int(data.size), d_rec.data_ptr(), d_n.data_ptr(), cap)
+            torch.cuda.synchronize()
+            recs, _, n = oracle.route(data, 8)
+            eb, er, ec = oracle.pack_by_owner(data, recs, 1)
+            assert np.array_equal(rb.cpu().numpy(), eb)
+            assert np.array_equal(rr.cpu().numpy().view(pkg.RECORD_DTYPE), er)
+            assert rc.cpu().tolist() == ec.tolist()
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,119 @@
+"""Multi-rank regroup on CPU with gloo: the product's exchange step
+(statsd-router_amd/regroup.py: all-to-all of split sizes, packed bytes and records, offset rebase)
+between world_size 2 and 3 process groups. The pack input comes from the oracle's restatement of
+sr_pack_by_owner (the HIP pack itself is checked against it in test_gpu_regroup.py)."""
+from __future__ import annotations
+
+import importlib
+import os
+import socket
+import sys
+import traceback
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import REPO
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _inputs(pkg, oracle, rank, n_shards, alive):
+    if rank == 2:   # a rank with nothing valid to send
+        data = np.frombuffer(pkg.frame_datagrams([b"no colon here\n", b"x\n", b"AAAA" * 400]), dtype=np.uint8)
+    else:
+        data = pkg.gen_stream(150_000 + 50_000 * rank, [64, 256, 1024], seed=77 + rank, p_invalid=0.1).data
+    recs, _, n = oracle.route(data, n_shards, alive)
+    return data, recs
+
+
+def _worker(rank, world, port, n_shards, q):
+    try:
+        sys.path.insert(0, REPO)
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pkg = importlib.import_module("statsd-router_amd")
+        rg = importlib.import_module("statsd-router_amd.regroup")
+        import sr_oracle as oracle
+
+        alive = [0 if k % 7 == 3 else 1 for k in range(n_shards)]
+        data, recs = _inputs(pkg, oracle, rank, n_shards, alive)
+        pb, pr, cnt = oracle.pack_by_owner(data, recs, world)
+        rb, rr, rc = rg.exchange_packed(torch.from_numpy(pb), torch.from_numpy(pr.view(np.int64)),
+                                        torch.from_numpy(cnt), None)
+        rb, rr = rb.numpy(), rr.numpy().view(pkg.RECORD_DTYPE)
+        # expected: every source's valid lines of the shards this rank owns, source by source
+        exp_lines, exp_routes = [], []
+        for s in range(world):
+            d, r = _inputs(pkg, oracle, s, n_shards, alive)
+            for x in r:
+                if x["route"] < 0xFFFD and x["route"] % world == rank:
+                    exp_lines.append(bytes(d[x["offset"]: x["offset"] + x["length"]]))
+                    exp_routes.append(int(x["route"]))
+        assert len(rr) == len(exp_lines), (len(rr), len(exp_lines))
+        got = [bytes(rb[x["offset"]: x["offset"] + x["length"]]) for x in rr]
+        assert got == exp_lines
+        assert [int(x) for x in rr["route"]] == exp_routes
+        assert all(x["offset"] % 4 == 0 for x in rr)
+        assert int(rc[:, 0].sum()) == len(exp_lines) and int(rc[:, 1].sum()) == rb.size
+        dist.destroy_process_group()
+        q.put((rank, None))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world,n_shards", [(2, 64), (3, 16), (2, 1)])
+def test_regroup_exchange_gloo(world, n_shards):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_shards, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            rank, err = q.get(timeout=240)
+            res[rank] = err
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    errs = {r: e for r, e in res.items() if e}
+    assert not errs, "\n".join(f"rank {r}:\n{e}" for r, e in errs.items())
+
+
+def test_pack_oracle_layout(pkg, oracle):
+    """The pack restatement itself: chunks by owner, input order, 4-byte aligned, zero fill."""
+    data = pkg.gen_stream(40_000, [64, 256], seed=5, p_invalid=0.2).data
+    recs, _, n = oracle.route(data, 10, [1] * 10)
+    pb, pr, cnt = oracle.pack_by_owner(data, recs, 4)
+    starts = np.concatenate([[0], np.cumsum(cnt[:, 1])])
+    k = 0
+    for o in range(4):
+        mine = [x for x in recs if x["route"] < 0xFFFD and x["route"] % 4 == o]
+        assert cnt[o, 0] == len(mine)
+        pos = 0
+        for x in mine:
+            y = pr[k]
+            k += 1
+            assert y["route"] == x["route"] and y["length"] == x["length"] and y["offset"] == pos
+            a = starts[o] + pos
+            assert bytes(pb[a: a + x["length"]]) == bytes(data[x["offset"]: x["offset"] + x["length"]])
+            pad = (-int(x["length"])) % 4
+            assert not pb[a + x["length"]: a + x["length"] + pad].any()
+            pos += int(x["length"]) + pad
+        assert pos == cnt[o, 1]
+    assert k == len(pr) == int(cnt[:, 0].sum())
