@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--per-launch", type=int, default=16,
                     help="batches routed per kernel launch (sr_route_device_many; 1 = sr_route_device)")
     ap.add_argument("--dead", type=float, default=0.0, help="fraction of dead downstreams")
+    ap.add_argument("--regroup", default="auto", choices=["auto", "on", "off"],
+                    help="classify + all-to-all regroup leg (auto: on when more than one GPU)")
+    ap.add_argument("--regroup-steps", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -60,6 +63,11 @@ def parse():
 
 def main():
     args = parse()
+    # The contract is ONE JSON line on stdout. Libraries (RCCL's version banner, HIP runtime notes)
+    # write to fd 1 as well: point fd 1 at stderr and keep a private handle for the result line.
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+    sys.stdout = sys.stderr
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -251,11 +259,63 @@ def main():
 
         if not args.no_e2e:
             result["e2e"] = e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M)
+    if args.regroup == "on" or (args.regroup == "auto" and world > 1):
+        rg = regroup_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, B, max_lines, dev, world,
+                         args.regroup_steps)
+        if rank == 0:
+            result["regroup"] = rg
     router.close()
     if rank == 0:
-        print(json.dumps(result), flush=True)
-    if world > 1:
+        print(json.dumps(result), file=json_out, flush=True)
+    if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def regroup_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, B, max_lines, dev, world, steps):
+    """Classify + regroup: per batch, route, pack by owner GPU (shard % G) and
+    all-to-all the packed lines and records (RCCL over xGMI). Not graph-captured: the split sizes
+    go through the host. Timed like the main region (barrier + synchronize, max over ranks)."""
+    rg_mod = importlib.import_module("statsd-router_amd.regroup")
+    if world == 1 and not dist.is_initialized():
+        dist.init_process_group("nccl", store=dist.TCPStore("127.0.0.1", 0, 1, True), rank=0, world_size=1)
+    reg = rg_mod.Regrouper(pkg, router, batch_bytes, max_lines)
+    d_rec = torch.empty(max_lines, dtype=torch.int64, device=dev)
+    d_n = torch.zeros(1, dtype=torch.int64, device=dev)
+    base = d_in.data_ptr()
+
+    def step(i):
+        b = i % B
+        router.route_device(base + b * batch_bytes, sizes[b], d_rec.data_ptr(), max_lines, None, d_n.data_ptr())
+        rb, rr, rc = reg(base + b * batch_bytes, sizes[b], d_rec.data_ptr(), d_n.data_ptr(), max_lines)
+        return int(rr.numel()), int(rb.numel()), int(reg.counts[:, 1].sum().item() - reg.counts[dist.get_rank(), 1].item())
+
+    with torch.cuda.stream(stream):
+        for i in range(2):
+            step(i)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        recv_lines = recv_bytes = sent_off = 0
+        for i in range(steps):
+            a, b_, c = step(i)
+            recv_lines += a
+            recv_bytes += b_
+            sent_off += c
+        torch.cuda.synchronize()
+        dist.barrier()
+        wall = time.perf_counter() - t0
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    tot = torch.tensor([sum(lines[i % B] for i in range(steps)), recv_lines, recv_bytes, sent_off],
+                       dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    w = float(t[0])
+    return {"value": round(float(tot[0]) / w / 1e6, 3), "unit": "M metrics/s",
+            "steps_per_gpu": steps, "ms_per_step": round(w * 1e3 / steps, 4),
+            "lines_regrouped": int(tot[1]), "bytes_regrouped": int(tot[2]),
+            "bytes_sent_to_other_gpus_per_s": round(float(tot[3]) / w / 1e9, 3),
+            "note": (f"route + sr_pack_by_owner + all-to-all (split sizes, packed lines, records) per 16 MiB batch "
+                     f"over {world} GPU(s); owner = shard % {world}; host round trip for the split sizes")}
 
 
 def e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M, groups=24):
