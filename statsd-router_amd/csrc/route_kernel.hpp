@@ -193,6 +193,22 @@ __device__ __forceinline__ uint32_t eq_mask16(uint4 v, uint32_t pat) {
            (eq_mask4(v.w, pat) << 12);
 }
 
+// 0x80 in every byte of x equal to the byte replicated in pat, 0 elsewhere (exact, 5 VALU ops)
+__device__ __forceinline__ uint32_t eq_flags(uint32_t x, uint32_t pat) {
+    const uint32_t t = x ^ pat;
+    return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+}
+
+// 16-bit mask (bit i = byte i) of the bytes of a 16-byte piece equal to pat. The 0x80 flags of
+// two dwords are packed by two v_dot4_u32_u8 with byte weights 1..128 (= 128 x the 8-bit mask).
+__device__ __forceinline__ uint32_t eq_mask16_dot(uint4 v, uint32_t pat) {
+    uint32_t lo = __builtin_amdgcn_udot4(eq_flags(v.x, pat), 0x08040201u, 0u, false);
+    lo = __builtin_amdgcn_udot4(eq_flags(v.y, pat), 0x80402010u, lo, false);
+    uint32_t hi = __builtin_amdgcn_udot4(eq_flags(v.z, pat), 0x08040201u, 0u, false);
+    hi = __builtin_amdgcn_udot4(eq_flags(v.w, pat), 0x80402010u, hi, false);
+    return (lo + (hi << 8)) >> 7;
+}
+
 // number of bytes equal to the replicated pattern
 __device__ __forceinline__ uint32_t eq_count4(uint32_t x, uint32_t pat) {
     const uint32_t t = x ^ pat;
@@ -377,8 +393,15 @@ struct SmemT {
     static constexpr int kRows = (kHalo + kTileB) / 64;
     static constexpr int kWords = kRows * 17 + 20;
     uint32_t img[kWords];
-    int32_t lend[kWin + 1];          // per staged line: tile position of its '\n'; slot 0 = previous
-    int32_t lcol[kWin + 1];          // per staged line: first ':' in the tile part (kNone if none)
+    union {
+        // load -> mask phase: per 16-byte piece P of the tile, its '\n' mask (low 16 bits) and
+        // ':' mask (high 16 bits), computed from the load registers
+        uint32_t pm[BLOCK * 4];
+        struct {
+            int32_t lend[kWin + 1];  // per staged line: tile position of its '\n'; slot 0 = previous
+            int32_t lcol[kWin + 1];  // per staged line: first ':' in the tile part (kNone if none)
+        };
+    };
     uint64_t wave_seg[kWaves];
     uint64_t wave_pre[kWaves];       // exclusive line state of each wave
     uint32_t wave_cnt[kWaves];
@@ -455,8 +478,8 @@ __device__ uint32_t count_tile_wave(uint32_t nbytes, __amdgpu_buffer_rsrc_t rsrc
 }
 
 // Exclusive line prefix of tile t: decoupled look-back by ONE wave,
-// 256 predecessors per round, stopping at the nearest inclusive prefix. Every lane returns the same value.
-constexpr int kLookPer = 4;   // predecessors per lane per look-back round
+// kLookPer x 64 predecessors per round, stopping at the nearest inclusive prefix. Every lane returns the same value.
+constexpr int kLookPer = 4;   // predecessors per lane per look-back round (256 per round)
 
 // First round of status loads, issued early so their latency hides behind the mask pass.
 __device__ __forceinline__ void look_back_prefetch(const uint64_t *status, uint32_t t, int lane,
@@ -487,7 +510,12 @@ __device__ uint32_t look_back_wave(const uint64_t *status, uint32_t nbytes, __am
             need[k] = in && !((uint32_t)(st[k] >> 34) == ep && ((st[k] >> 32) & 3u) != 0);
         }
         round0 = false;
-        if (!__ballot(need[0] | need[1] | need[2] | need[3])) goto polled;
+        {
+            bool any = false;
+#pragma unroll
+            for (int k = 0; k < kPer; ++k) any |= need[k];
+            if (!__ballot(any)) goto polled;
+        }
         for (int spin = 0;; ++spin) {
             bool pending = false;
 #pragma unroll
@@ -582,8 +610,9 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
         img_put16(sm, tid * 16, hv);
     }
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
-    // coalesced tile load: wave instruction k of thread tid covers bytes k*BLOCK*16 + tid*16;
-    // the '\n' count is taken from the registers so the tile's aggregate can be published early
+    // coalesced tile load: wave instruction k of thread tid covers piece P = k*BLOCK + tid (bytes
+    // 16P ..); the '\n' / ':' masks of the piece are taken from the registers (-> sm.pm) and the
+    // '\n' count with them, so the tile's aggregate can be published early
     {
         uint4 v[4];
         uint32_t cnt = 0;
@@ -592,8 +621,10 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             img_put16(sm, kHalo + 16 * (k * BLOCK + tid), v[k]);
-            cnt += eq_count4(v[k].x, 0x0A0A0A0Au) + eq_count4(v[k].y, 0x0A0A0A0Au) +
-                   eq_count4(v[k].z, 0x0A0A0A0Au) + eq_count4(v[k].w, 0x0A0A0A0Au);
+            const uint32_t nl = eq_mask16_dot(v[k], 0x0A0A0A0Au);
+            const uint32_t cl = eq_mask16_dot(v[k], 0x3A3A3A3Au);
+            sm.pm[k * BLOCK + tid] = nl | (cl << 16);
+            cnt += __popc(nl);
         }
         cnt = wave_add32(cnt);
         if (lane == 0) sm.wave_cnt[wave] = cnt;
@@ -608,7 +639,9 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
         const uint64_t st = mk_status(epoch, t == 0 ? kFlagIncl : kFlagAgg, tile_count);
         __hip_atomic_store(&status[t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    uint64_t lb_first[kLookPer] = {0ull, 0ull, 0ull, 0ull};
+    uint64_t lb_first[kLookPer];
+#pragma unroll
+    for (int k = 0; k < kLookPer; ++k) lb_first[k] = 0ull;
     if (wave == 0 && !(ABL & ABL_NO_LOOKBACK)) look_back_prefetch(status, t, lane, lb_first);
     if (ABL & ABL_LOAD_ONLY) {
         if (tid == 0 && t == ntiles - 1) *bd.n_out = tile_count;
@@ -616,17 +649,16 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
     } else {
     // ---- per lane: '\n' / ':' masks of its 64 contiguous bytes, segmented line-state scan -------
     const int o = tid * kLaneBytes;   // tile position of the lane's first byte
-    uint64_t nlm = 0, clm = 0;        // bit i: byte o+i is '\n' / ':'
-#pragma unroll
-    for (int pc = 0; pc < 4; ++pc) {
-        const uint4 v = img_get16(sm, kHalo + 64 * tid + 16 * pc);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int sh = 16 * pc + 4 * k;
-            nlm |= (uint64_t)eq_mask4(w[k], 0x0A0A0A0Au) << sh;
-            clm |= (uint64_t)eq_mask4(w[k], 0x3A3A3A3Au) << sh;
-        }
+    uint64_t nlm, clm;                // bit i: byte o+i is '\n' / ':'
+    {
+        // the lane's pieces 4 tid .. 4 tid + 3 (one 16-byte LDS read); v_perm gathers the halves
+        const uint4 q = *(const uint4 *)&sm.pm[4 * tid];
+        const uint32_t n_lo = __builtin_amdgcn_perm(q.y, q.x, 0x05040100u);
+        const uint32_t n_hi = __builtin_amdgcn_perm(q.w, q.z, 0x05040100u);
+        const uint32_t c_lo = __builtin_amdgcn_perm(q.y, q.x, 0x07060302u);
+        const uint32_t c_hi = __builtin_amdgcn_perm(q.w, q.z, 0x07060302u);
+        nlm = ((uint64_t)n_hi << 32) | n_lo;
+        clm = ((uint64_t)c_hi << 32) | c_lo;
     }
     const int ncnt = __popcll(nlm);
     uint64_t seg;

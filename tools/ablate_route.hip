@@ -146,31 +146,14 @@ int main(int argc, char **argv) {
             if (round == 0) rows.push_back(Row{name, {0, 0, 0}});
             rows[i++].us[round] = us;
         };
-        put("b1024_full_s1", time_variant<1024, ABL_NONE>(c, 1, reps));
-        put("b1024_m2", time_variant<1024, ABL_NONE>(c, 1, reps, 2));
-        put("b1024_m4", time_variant<1024, ABL_NONE>(c, 1, reps, 4));
-        put("b1024_m8", time_variant<1024, ABL_NONE>(c, 1, reps, 8));
-        put("b1024_m16", time_variant<1024, ABL_NONE>(c, 1, reps, 16));
-        put("b512_m4", time_variant<512, ABL_NONE>(c, 1, reps, 4));
-        put("b512_m8", time_variant<512, ABL_NONE>(c, 1, reps, 8));
         put("b512_m16", time_variant<512, ABL_NONE>(c, 1, reps, 16));
-        put("b256_m8", time_variant<256, ABL_NONE>(c, 1, reps, 8));
+        put("b1024_m16", time_variant<1024, ABL_NONE>(c, 1, reps, 16));
         put("b256_m16", time_variant<256, ABL_NONE>(c, 1, reps, 16));
-        put("b512_m4_s4", time_variant<512, ABL_NONE>(c, 4, reps, 4));
-        put("b512_load_only_m8", time_variant<512, ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps, 8));
-        put("b1024_load_only_m8", time_variant<1024, ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps, 8));
-        put("b512_full_s1", time_variant<512, ABL_NONE>(c, 1, reps));
-        put("b256_full_s1", time_variant<256, ABL_NONE>(c, 1, reps));
-        put("b1024_full_s2", time_variant<1024, ABL_NONE>(c, 2, reps));
-        put("b512_full_s2", time_variant<512, ABL_NONE>(c, 2, reps));
-        put("b512_full_s4", time_variant<512, ABL_NONE>(c, 4, reps));
-        put("b256_full_s4", time_variant<256, ABL_NONE>(c, 4, reps));
-        put("b512_no_lookback", time_variant<512, ABL_NO_LOOKBACK>(c, 1, reps));
-        put("b512_no_lines", time_variant<512, ABL_NO_LINES>(c, 1, reps));
-        put("b512_no_prologue", time_variant<512, ABL_NO_PROLOGUE>(c, 1, reps));
-        put("b512_load_only", time_variant<512, ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps));
-        put("b512_no_lines_s4", time_variant<512, ABL_NO_LINES>(c, 4, reps));
-        put("b512_load_only_s4", time_variant<512, ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 4, reps));
+        put("b512_m16_no_lookback", time_variant<512, ABL_NO_LOOKBACK>(c, 1, reps, 16));
+        put("b512_m16_no_lines", time_variant<512, ABL_NO_LINES>(c, 1, reps, 16));
+        put("b512_m16_no_prologue", time_variant<512, ABL_NO_PROLOGUE>(c, 1, reps, 16));
+        put("b512_m16_load_only", time_variant<512, ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps, 16));
+        put("b512_m1", time_variant<512, ABL_NONE>(c, 1, reps, 1));
         put("read_kernel_s1", time_variant<256, 0xFFFFu>(c, 1, reps));
         put("read_kernel_s4", time_variant<256, 0xFFFFu>(c, 4, reps));
     }

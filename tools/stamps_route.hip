@@ -78,6 +78,49 @@ void run(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size_t> &
            med(ph[3]), med(ph[4]), med(ph[5]));
 }
 
+// one launch over all L batches (the product's multi-batch mode): per-phase medians over every
+// workgroup of the launch, plus the launch span
+template <int BLOCK>
+void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size_t> &sizes, sr_record *d_out,
+              size_t max_lines, uint64_t *d_n, uint64_t *d_dbg, hipStream_t s, uint32_t line_len) {
+    const int L = (int)batches.size();
+    const uint32_t T = BLOCK * kLaneBytes;
+    uint32_t total = 0;
+    for (int i = 0; i < L; ++i) total += (uint32_t)((sizes[i] + T - 1) / T);
+    std::vector<uint64_t> h((size_t)total * 8);
+    auto launch = [&]() {
+        RouteParams p = ds.params();
+        for (int i = 0; i < L; ++i)
+            DeviceState::add_batch(p, batches[i], sizes[i], d_out + (size_t)i * max_lines, max_lines, nullptr, d_n + i);
+        p.dbg = d_dbg;
+        launch_route<BLOCK, ABL_STAMPS>(ds, p, s);
+    };
+    for (int w = 0; w < 3; ++w) launch();
+    CK(hipStreamSynchronize(s));
+    launch();
+    CK(hipStreamSynchronize(s));
+    CK(hipMemcpy(h.data(), d_dbg, h.size() * 8, hipMemcpyDeviceToHost));
+    std::vector<double> ph[6];
+    uint64_t s0 = ~0ull, e1 = 0;
+    for (uint32_t b = 0; b < total; ++b) {
+        const uint64_t *d = h.data() + (size_t)b * 8;
+        s0 = std::min(s0, d[0]);
+        e1 = std::max(e1, d[6]);
+        const double u = 0.01;
+        ph[0].push_back((d[1] - d[0]) * u);
+        ph[1].push_back((d[2] - d[1]) * u);
+        ph[2].push_back((d[3] - d[2]) * u);
+        ph[3].push_back((d[4] - d[2]) * u);
+        ph[4].push_back((d[5] - d[4]) * u);
+        ph[5].push_back((d[6] - d[0]) * u);
+    }
+    printf("{\"mode\": \"%d batches per launch\", \"block\": %d, \"line_len\": %u, \"tiles\": %u, \"span_us\": %.2f, "
+           "\"median_us\": {\"load\": %.2f, \"masks_scan\": %.2f, \"lookback\": %.2f, \"to_staged\": %.2f, "
+           "\"hash_records\": %.2f, \"lifetime\": %.2f}}\n",
+           L, BLOCK, line_len, total, (e1 - s0) * 0.01, med(ph[0]), med(ph[1]), med(ph[2]), med(ph[3]), med(ph[4]),
+           med(ph[5]));
+}
+
 int main(int argc, char **argv) {
     const int L = 16;
     const size_t batch = 16u << 20;
@@ -100,13 +143,15 @@ int main(int argc, char **argv) {
     }
     sr_record *d_out;
     uint64_t *d_n, *d_dbg;
-    CK(hipMalloc(&d_out, nl * sizeof(sr_record)));
-    CK(hipMalloc(&d_n, 8));
+    CK(hipMalloc(&d_out, (size_t)L * nl * sizeof(sr_record)));
+    CK(hipMalloc(&d_n, 8 * L));
     CK(hipMalloc(&d_dbg, (size_t)L * 4096 * 8 * 8));
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     run<1024>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
     run<512>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
     run<256>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
+    run_many<512>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
+    run_many<1024>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
     return 0;
 }
