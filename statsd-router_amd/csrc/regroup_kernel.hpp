@@ -44,17 +44,6 @@ struct PackParams {
 
 __device__ __forceinline__ uint32_t pack_len4(uint32_t len) { return (len + 3u) & ~3u; }
 
-// inclusive wave scan of a u32 (DPP; no LDS)
-__device__ __forceinline__ uint32_t wave_incl_add32(uint32_t v) {
-    v += dpp32<kDppRowShr1>(0u, v);
-    v += dpp32<kDppRowShr2>(0u, v);
-    v += dpp32<kDppRowShr4>(0u, v);
-    v += dpp32<kDppRowShr8>(0u, v);
-    v += dpp32<kDppRowBcast15, 0xA>(0u, v);
-    v += dpp32<kDppRowBcast31, 0xC>(0u, v);
-    return v;
-}
-
 // owner of record r, or -1 when the line goes to no shard
 __device__ __forceinline__ int pack_owner(const sr_record &r, uint32_t n_owners) {
     return r.route < SR_ROUTE_INVALID_LENGTH ? (int)(r.route % n_owners) : -1;

@@ -56,6 +56,7 @@ struct DeviceState {
     uint64_t *d_kpow = nullptr;
     Control *d_ctl = nullptr;
     uint64_t *d_status = nullptr;
+    uint64_t *d_bases = nullptr;
     PendingLine *d_pending = nullptr;
 
     int init(size_t max_batch_bytes, uint32_t n_downstreams) {
@@ -71,6 +72,8 @@ struct DeviceState {
         if (hipMalloc(&d_kpow, kPowTable * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&d_ctl, sizeof(Control)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&d_status, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+        if (hipMalloc(&d_bases, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+        if (hipMemset(d_bases, 0, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -EIO;
         if (hipMemset(d_ctl, 0, sizeof(Control)) != hipSuccess) return -EIO;
         if (hipMemset(d_status, 0, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -EIO;
         std::vector<Magic> mg(n_downstreams + 1);
@@ -106,6 +109,7 @@ struct DeviceState {
         (void)hipFree(d_kpow);
         (void)hipFree(d_ctl);
         (void)hipFree(d_status);
+        (void)hipFree(d_bases);
         (void)hipFree(d_pending);
         free(h_alive);
         d_alive = nullptr;
@@ -113,6 +117,7 @@ struct DeviceState {
         d_kpow = nullptr;
         d_ctl = nullptr;
         d_status = nullptr;
+        d_bases = nullptr;
         d_pending = nullptr;
         h_alive = nullptr;
     }
@@ -154,6 +159,7 @@ struct DeviceState {
         p.kpow = d_kpow;
         p.ctl = d_ctl;
         p.status = d_status;
+        p.bases = d_bases;
         p.pending = d_pending;
         p.dbg = nullptr;
         return p;
@@ -217,9 +223,9 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
     }
     if (tiles == 0) return 0;
     if (tiles > ds.max_tiles) return -EINVAL;
-    p.total_tiles = tiles;
+    p.total_blocks = p.nb + tiles;   // scanners first, then the tiles
     if (ds.wide() && hipMemsetAsync(&ds.d_ctl->pending, 0, sizeof(uint32_t), stream) != hipSuccess) return -EIO;
-    hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(tiles), dim3(BLOCK), 0, stream, p);
+    hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     if (hipGetLastError() != hipSuccess) return -EIO;
     if (ds.wide()) {
         static bool attr_set = false;

@@ -128,7 +128,7 @@ struct BatchDesc {
 
 struct RouteParams {
     uint32_t nb;             // batches in this launch
-    uint32_t total_tiles;    // grid size
+    uint32_t total_blocks;   // grid size: nb scanners + every batch's tiles
     uint32_t nds;            // number of downstreams
     uint32_t dead;           // dead downstreams in the alive snapshot
     uint32_t pending_cap;
@@ -137,7 +137,8 @@ struct RouteParams {
     const Magic *magic;      // [0..nds], index i -> divisor i
     const uint64_t *kpow;    // kPowTable entries: K^i, K^(64 i), K^-i (i < 64)
     Control *ctl;
-    uint64_t *status;        // per-tile look-back granules
+    uint64_t *status;        // per-tile '\n' count granules {epoch, flag, count} (written by the tile)
+    uint64_t *bases;         // per-tile first-record granules {epoch, flag, base} (written by the scanner)
     PendingLine *pending;
     uint64_t *dbg;           // ABL_STAMPS builds only: 8 timestamps per tile
     BatchDesc b[kMaxBatches];
@@ -309,6 +310,17 @@ __device__ __forceinline__ uint32_t wave_add32(uint32_t v) {   // sum over the w
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
+// inclusive wave scan of a u32 (DPP; no LDS)
+__device__ __forceinline__ uint32_t wave_incl_add32(uint32_t v) {
+    v += dpp32<kDppRowShr1>(0u, v);
+    v += dpp32<kDppRowShr2>(0u, v);
+    v += dpp32<kDppRowShr4>(0u, v);
+    v += dpp32<kDppRowShr8>(0u, v);
+    v += dpp32<kDppRowBcast15, 0xA>(0u, v);
+    v += dpp32<kDppRowBcast31, 0xC>(0u, v);
+    return v;
+}
+
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
     const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, lane);
     const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), lane);
@@ -477,94 +489,101 @@ __device__ uint32_t count_tile_wave(uint32_t nbytes, __amdgpu_buffer_rsrc_t rsrc
     return (uint32_t)wave_sum64(c);
 }
 
-// Exclusive line prefix of tile t: decoupled look-back by ONE wave,
-// kLookPer x 64 predecessors per round, stopping at the nearest inclusive prefix. Every lane returns the same value.
-constexpr int kLookPer = 4;   // predecessors per lane per look-back round (256 per round)
+// ---- record numbering: one scanner wave per batch --------------------------------------------
+// Blocks 0 .. nb-1 of a launch are scanners, one per batch; they are dispatched before every tile.
+// A tile publishes its '\n' count straight after its loads (status granule, never waits for
+// anything); the scanner of its batch walks the batch's tiles in order, 64 per round, and
+// publishes each tile's first record index (bases granule) as soon as the counts of all its
+// predecessors are in. A tile needs its base only when it writes its records, after hashing.
+// A tile whose count has not appeared within the spin budget is counted by the scanner itself,
+// so the scan completes whatever the dispatch order.
+constexpr uint32_t kFlagBase = 2u;
 
-// First round of status loads, issued early so their latency hides behind the mask pass.
-__device__ __forceinline__ void look_back_prefetch(const uint64_t *status, uint32_t t, int lane,
-                                                   uint64_t (&first)[kLookPer]) {
-#pragma unroll
-    for (int k = 0; k < kLookPer; ++k) {
-        const int64_t idx = (int64_t)t - 1 - lane - 64 * k;
-        first[k] = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-    }
+__device__ __forceinline__ bool granule_ok(uint64_t st, uint32_t ep, uint32_t flag) {
+    return (uint32_t)(st >> 34) == ep && ((st >> 32) & 3u) == flag;
 }
 
 template <int BLOCK>
-__device__ uint32_t look_back_wave(const uint64_t *status, uint32_t nbytes, __amdgpu_buffer_rsrc_t rsrc, uint32_t t,
-                                   uint32_t epoch, int lane, const uint64_t (&first)[kLookPer]) {
-    constexpr int kPer = kLookPer;
-    uint64_t acc = 0;
-    int64_t hi = t;
+__device__ void scan_batch(const RouteParams &p, const BatchDesc &bd, uint32_t epoch, int lane) {
+    const uint64_t *status = p.status + bd.tile0;
+    uint64_t *bases = p.bases + bd.tile0;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
     const uint32_t ep = epoch & 0x3FFFFFFFu;
-    bool round0 = true;
-    while (hi > 0) {
-        const int64_t lo = hi - 64 * kPer > 0 ? hi - 64 * kPer : 0;
-        uint64_t st[kPer];
-        bool need[kPer];
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const bool in = hi - 1 - lane - 64 * k >= lo;
-            st[k] = round0 ? first[k] : 0ull;
-            need[k] = in && !((uint32_t)(st[k] >> 34) == ep && ((st[k] >> 32) & 3u) != 0);
-        }
-        round0 = false;
-        {
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < kPer; ++k) any |= need[k];
-            if (!__ballot(any)) goto polled;
-        }
+    uint32_t run = 0;
+    for (uint32_t c = 0; c < bd.ntiles; c += 64) {
+        const uint32_t tt = c + lane;
+        const bool in = tt < bd.ntiles;
+        uint32_t cnt = 0;
+        bool need = in;
         for (int spin = 0;; ++spin) {
-            bool pending = false;
-#pragma unroll
-            for (int k = 0; k < kPer; ++k) {
-                if (!need[k]) continue;
-                st[k] = __hip_atomic_load(&status[hi - 1 - lane - 64 * k], __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-                need[k] = !((uint32_t)(st[k] >> 34) == ep && ((st[k] >> 32) & 3u) != 0);
-                pending |= need[k];
-            }
-            if (!__ballot(pending)) break;
-            if (spin >= kSpinBudget) break;
-            __builtin_amdgcn_s_sleep(2);
-        }
-    polled:
-        // predecessors still silent: count their tiles here (never needed under in-order
-        // dispatch; it makes progress independent of dispatch order)
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            uint64_t mask = __ballot(need[k]);
-            while (mask) {
-                const int L = __builtin_ctzll(mask);
-                mask &= mask - 1;
-                const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(hi - 1 - L - 64 * k), L);
-                const uint32_t cnt = count_tile_wave<BLOCK>(nbytes, rsrc, m, lane);
-                if (lane == L) {
-                    st[k] = mk_status(epoch, kFlagAgg, cnt);
-                    need[k] = false;
+            if (need) {
+                const uint64_t st = __hip_atomic_load(&status[tt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (granule_ok(st, ep, kFlagAgg)) {
+                    cnt = (uint32_t)st;
+                    need = false;
                 }
             }
+            uint64_t missing = __ballot(need);
+            if (!missing) break;
+            if (spin >= kSpinBudget) {   // silent tiles: count them here
+                while (missing) {
+                    const int L = __builtin_ctzll(missing);
+                    missing &= missing - 1;
+                    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)tt, L);
+                    const uint32_t c2 = count_tile_wave<BLOCK>(bd.nbytes, rsrc, m, lane);
+                    if (lane == L) {
+                        cnt = c2;
+                        need = false;
+                    }
+                }
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
         }
-        int near = -1;
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int64_t idx = hi - 1 - lane - 64 * k;
-            if (idx >= lo && ((st[k] >> 32) & 3u) == kFlagIncl) near = max(near, (int)idx);
-        }
-        near = wave_max_i32(near);
-        uint64_t part = 0;
-#pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-            const int64_t idx = hi - 1 - lane - 64 * k;
-            if (idx >= lo && idx >= near) part += st[k] & 0xFFFFFFFFull;
-        }
-        acc += wave_sum64(part);
-        if (near >= 0) break;
-        hi = lo;
+        const uint32_t incl = wave_incl_add32(cnt);
+        if (in)
+            __hip_atomic_store(&bases[tt], mk_status(epoch, kFlagBase, run + incl - cnt), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     }
-    return (uint32_t)acc;
+    if (lane == 0) *bd.n_out = run;
+}
+
+// a tile's first record index, from its scanner (per lane; the lanes of a wave read one address).
+// Fallback after a long wait (never taken when blocks are dispatched in order): count the '\n'
+// bytes before the tile directly.
+__device__ uint32_t wait_base(const uint64_t *slot, uint32_t epoch, __amdgpu_buffer_rsrc_t rsrc, uint32_t T0) {
+    const uint32_t ep = epoch & 0x3FFFFFFFu;
+    for (uint32_t spin = 0; spin < (1u << 22); ++spin) {
+        const uint64_t st = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (granule_ok(st, ep, kFlagBase)) return (uint32_t)st;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    uint32_t n = 0;
+    for (uint32_t off = 0; off < T0; off += 4)
+        n += eq_count4(__builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0), 0x0A0A0A0Au);
+    return n;
+}
+
+// Arrivals: every block adds itself to a sharded counter (no return value, nothing waits); the
+// last block waits until all have arrived, then resets the counters and advances the epoch.
+// Every block read the epoch before arriving, so none of this launch can see the new one.
+__device__ void arrive(const RouteParams &p, uint32_t blk, uint32_t epoch) {
+    __hip_atomic_fetch_add(&p.ctl->done[blk & 7u][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blk != p.total_blocks - 1) return;
+    for (uint32_t spin = 0; spin < (1u << 26); ++spin) {
+        uint32_t n = 0;
+#pragma unroll
+        for (int s8 = 0; s8 < 8; ++s8)
+            n += __hip_atomic_load(&p.ctl->done[s8][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (n >= p.total_blocks) break;
+        __builtin_amdgcn_s_sleep(2);
+    }
+#pragma unroll
+    for (int s8 = 0; s8 < 8; ++s8)
+        __hip_atomic_store(&p.ctl->done[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&p.ctl->epoch, epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int BLOCK>
@@ -586,7 +605,13 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    const uint32_t g = blockIdx.x;
+    if (blockIdx.x < p.nb) {   // scanner of batch blockIdx.x (wave 0; no barriers on this path)
+        const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (wave == 0) scan_batch<BLOCK>(p, p.b[blockIdx.x], ep0, lane);
+        if (tid == 0) arrive(p, blockIdx.x, ep0);
+        return;
+    }
+    const uint32_t g = blockIdx.x - p.nb;   // tile index within the launch
     // the batch of this tile (uniform; at most kMaxBatches scalar compares)
     uint32_t bi = 0;
     for (uint32_t k = 1; k < p.nb; ++k)
@@ -595,6 +620,7 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
     const uint8_t *const bytes = bd.bytes;
     const uint32_t nbytes = bd.nbytes, ntiles = bd.ntiles;
     uint64_t *const status = p.status + bd.tile0;
+    const uint64_t *const base_slot = p.bases + bd.tile0 + (g - bd.tile0);
     const uint32_t t = g - bd.tile0;   // tile index within the batch
     const int64_t T0 = (int64_t)t * kTileB;
     const __amdgpu_buffer_rsrc_t rsrc =
@@ -635,16 +661,11 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
     uint32_t tile_count = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) tile_count += sm.wave_cnt[w];
-    if (tid == 0) {   // publish this tile's aggregate (tile 0: its inclusive prefix)
-        const uint64_t st = mk_status(epoch, t == 0 ? kFlagIncl : kFlagAgg, tile_count);
+    if (tid == 0) {   // publish this tile's '\n' count for the scanner
+        const uint64_t st = mk_status(epoch, kFlagAgg, tile_count);
         __hip_atomic_store(&status[t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    uint64_t lb_first[kLookPer];
-#pragma unroll
-    for (int k = 0; k < kLookPer; ++k) lb_first[k] = 0ull;
-    if (wave == 0 && !(ABL & ABL_NO_LOOKBACK)) look_back_prefetch(status, t, lane, lb_first);
     if (ABL & ABL_LOAD_ONLY) {
-        if (tid == 0 && t == ntiles - 1) *bd.n_out = tile_count;
         __syncthreads();
     } else {
     // ---- per lane: '\n' / ':' masks of its 64 contiguous bytes, segmented line-state scan -------
@@ -684,22 +705,7 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
     // empty range (lane 0): count 0, no '\n', no colon
     const uint64_t eseg = seg_combine(sm.wave_pre[wave], wave_shr1_64(sseg, (uint64_t)kNone));
 
-    // ---- wave 0: decoupled look-back for the tile's first record index -----------------------
-    if (wave == 0) {
-        uint32_t base = 0;
-        if (!(ABL & ABL_NO_LOOKBACK)) {
-            base = look_back_wave<BLOCK>(status, nbytes, rsrc, t, epoch, lane, lb_first);
-            if (lane == 0 && t > 0) {
-                const uint64_t st = mk_status(epoch, kFlagIncl, base + tile_count);
-                __hip_atomic_store(&status[t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        if (lane == 0) {
-            sm.base = base;
-            if (t == ntiles - 1) *bd.n_out = (uint64_t)base + tile_count;
-        }
-        stamp<ABL>(p, tid, g, 3);
-    }
+    if (tid == 0) stamp<ABL>(p, tid, g, 3);
     // ---- last wave: where the line that straddles into the tile starts, its first ':' ----------
     if (wave == kPreWave) {
         int64_t s_abs = 0;
@@ -754,6 +760,8 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
     const int lane_first = (int)(eseg >> 32);               // tile-local index of lane's 1st line
     const int open_fc = (int)((uint32_t)eseg & 0x1FFFFu);   // first ':' (in the tile) of the open line
     if (tid == 0) sm.lend[0] = 0;
+    uint32_t base = 0;                                        // first record index of the tile
+    bool have_base = (ABL & (ABL_NO_LOOKBACK | ABL_NO_LINES)) != 0;
     for (int wbase = 0; wbase < (int)tile_count; wbase += kWin) {
         // (1) stage (e, c) of the lane's lines that fall into this window
         if (nlm && lane_first + ncnt > wbase && lane_first < wbase + kWin) {
@@ -783,7 +791,6 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
         __syncthreads();
         if (wbase == 0) stamp<ABL>(p, tid, g, 4);
         if (!(ABL & ABL_NO_LINES)) {
-            const uint32_t base = sm.base;
             const int s_pre = sm.s_pre;
             const int c_pre = sm.c_pre;
             const int nwin = min(kWin, (int)tile_count - wbase);
@@ -816,6 +823,10 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
                     if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
                     else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
                     else route = probe_shard(h, p);                                                    // :145
+                    if (!have_base) {   // needed only now, after the hash: normally long published
+                        base = wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
+                        have_base = true;
+                    }
                     const uint32_t rec = base + (uint32_t)j;
                     if (rec < bd.max_records) {
                         if (route == kRoutePending) {
@@ -840,26 +851,7 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
     }
     stamp<ABL>(p, tid, g, 6);
 
-    // ---- arrivals: every workgroup adds itself (no return value, nothing waits); the last tile
-    // waits until all have arrived, then resets the counters and advances the epoch. Every
-    // workgroup read the epoch before arriving, so none of this launch can see the new one.
-    if (tid == 0) {
-        __hip_atomic_fetch_add(&p.ctl->done[g & 7u][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (g == p.total_tiles - 1) {
-            for (uint32_t spin = 0; spin < (1u << 26); ++spin) {
-                uint32_t n = 0;
-#pragma unroll
-                for (int s8 = 0; s8 < 8; ++s8)
-                    n += __hip_atomic_load(&p.ctl->done[s8][0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (n >= p.total_tiles) break;
-                __builtin_amdgcn_s_sleep(2);
-            }
-#pragma unroll
-            for (int s8 = 0; s8 < 8; ++s8)
-                __hip_atomic_store(&p.ctl->done[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&p.ctl->epoch, epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
+    if (tid == 0) arrive(p, blockIdx.x, epoch);
 }
 
 // Lines whose probe met more than kOverlay dead shards: run find_downstream (sr-main.c:86-117)
