@@ -505,47 +505,66 @@ __device__ __forceinline__ bool granule_ok(uint64_t st, uint32_t ep, uint32_t fl
 
 template <int BLOCK>
 __device__ void scan_batch(const RouteParams &p, const BatchDesc &bd, uint32_t epoch, int lane) {
+    constexpr int kGroups = 4;   // 64-tile groups polled per round
     const uint64_t *status = p.status + bd.tile0;
     uint64_t *bases = p.bases + bd.tile0;
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
     const uint32_t ep = epoch & 0x3FFFFFFFu;
     uint32_t run = 0;
-    for (uint32_t c = 0; c < bd.ntiles; c += 64) {
-        const uint32_t tt = c + lane;
-        const bool in = tt < bd.ntiles;
-        uint32_t cnt = 0;
-        bool need = in;
-        for (int spin = 0;; ++spin) {
-            if (need) {
+    uint32_t c = 0;      // first tile whose base is not yet published (multiple of 64)
+    int spin = 0;        // rounds without progress on group c
+    while (c < bd.ntiles) {
+        // one round trip: the counts of up to kGroups groups from c on
+        uint32_t cnt[kGroups];
+        bool have[kGroups];
+#pragma unroll
+        for (int k = 0; k < kGroups; ++k) {
+            const uint32_t tt = c + 64 * k + lane;
+            cnt[k] = 0;
+            have[k] = tt >= bd.ntiles;
+            if (!have[k]) {
                 const uint64_t st = __hip_atomic_load(&status[tt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (granule_ok(st, ep, kFlagAgg)) {
-                    cnt = (uint32_t)st;
-                    need = false;
+                    cnt[k] = (uint32_t)st;
+                    have[k] = true;
                 }
             }
-            uint64_t missing = __ballot(need);
-            if (!missing) break;
-            if (spin >= kSpinBudget) {   // silent tiles: count them here
-                while (missing) {
-                    const int L = __builtin_ctzll(missing);
-                    missing &= missing - 1;
-                    const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)tt, L);
-                    const uint32_t c2 = count_tile_wave<BLOCK>(bd.nbytes, rsrc, m, lane);
-                    if (lane == L) {
-                        cnt = c2;
-                        need = false;
-                    }
+        }
+        // head group still incomplete after the spin budget: count its silent tiles here
+        if (spin >= kSpinBudget) {
+            uint64_t missing = __ballot(!have[0]);
+            while (missing) {
+                const int L = __builtin_ctzll(missing);
+                missing &= missing - 1;
+                const uint32_t c2 = count_tile_wave<BLOCK>(bd.nbytes, rsrc, c + (uint32_t)L, lane);
+                if (lane == L) {
+                    cnt[0] = c2;
+                    have[0] = true;
                 }
-                break;
             }
+        }
+        // publish the complete groups in order
+        bool progress = false;
+#pragma unroll
+        for (int k = 0; k < kGroups; ++k) {
+            if (__ballot(!have[k])) break;
+            const uint32_t tt = c + lane;   // c has advanced by 64 per published group
+            const uint32_t incl = wave_incl_add32(cnt[k]);
+            if (tt < bd.ntiles)
+                __hip_atomic_store(&bases[tt], mk_status(epoch, kFlagBase, run + incl - cnt[k]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            c += 64;
+            progress = true;
+            if (c >= bd.ntiles) break;
+        }
+        if (progress) {
+            spin = 0;
+        } else {
+            ++spin;
             __builtin_amdgcn_s_sleep(1);
         }
-        const uint32_t incl = wave_incl_add32(cnt);
-        if (in)
-            __hip_atomic_store(&bases[tt], mk_status(epoch, kFlagBase, run + incl - cnt), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-        run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     }
     if (lane == 0) *bd.n_out = run;
 }

@@ -154,6 +154,10 @@ int main(int argc, char **argv) {
         put("b512_m16_no_prologue", time_variant<512, ABL_NO_PROLOGUE>(c, 1, reps, 16));
         put("b512_m16_load_only", time_variant<512, ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps, 16));
         put("b512_m1", time_variant<512, ABL_NONE>(c, 1, reps, 1));
+        put("b256_m16_no_lookback", time_variant<256, ABL_NO_LOOKBACK>(c, 1, reps, 16));
+        put("b256_m16_no_lines", time_variant<256, ABL_NO_LINES>(c, 1, reps, 16));
+        put("b256_m16_load_only", time_variant<256, ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps, 16));
+        put("b256_m1", time_variant<256, ABL_NONE>(c, 1, reps, 1));
         put("read_kernel_s1", time_variant<256, 0xFFFFu>(c, 1, reps));
         put("read_kernel_s4", time_variant<256, 0xFFFFu>(c, 4, reps));
     }

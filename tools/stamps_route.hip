@@ -152,6 +152,6 @@ int main(int argc, char **argv) {
     run<512>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
     run<256>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
     run_many<512>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
-    run_many<1024>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
+    run_many<256>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
     return 0;
 }
