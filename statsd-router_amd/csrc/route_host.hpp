@@ -183,7 +183,7 @@ struct DeviceState {
         b.hashes = d_hashes;
         b.n_out = d_n;
         b.max_records = (uint32_t)(max_records > 0xFFFFFFFFull ? 0xFFFFFFFFull : max_records);
-        b.tile0 = b.ntiles = 0;
+        b.tile0 = b.ntiles = b.sbase = b.cls = 0;
         return true;
     }
 
@@ -208,22 +208,36 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
     }
     RouteParams p = in;
     p.nb = 0;
-    uint32_t tiles = 0;
     for (uint32_t i = 0; i < in.nb; ++i) {
-        const BatchDesc &b = in.b[i];
-        if (b.nbytes == 0) {
-            if (hipMemsetAsync(b.n_out, 0, sizeof(uint64_t), stream) != hipSuccess) return -EIO;
+        if (in.b[i].nbytes == 0) {
+            if (hipMemsetAsync(in.b[i].n_out, 0, sizeof(uint64_t), stream) != hipSuccess) return -EIO;
             continue;
         }
-        BatchDesc &d = p.b[p.nb++];
-        d = b;
-        d.tile0 = tiles;
-        d.ntiles = (uint32_t)((b.nbytes + T - 1) / T);
-        tiles += d.ntiles;
+        p.b[p.nb++] = in.b[i];
     }
-    if (tiles == 0) return 0;
-    if (tiles > ds.max_tiles) return -EINVAL;
-    p.total_blocks = p.nb + tiles;   // scanners first, then the tiles
+    if (p.nb == 0) return 0;
+    // 8+ batches: each batch's tiles on one XCD class; its scanner (block j) shares that class
+    const bool xl = !(ABL & ABL_NO_XCD_LOCAL) && p.nb >= 8;
+    p.xcd_local = xl ? 1u : 0u;
+    uint32_t cls_tiles[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t sb = 0;
+    for (uint32_t j = 0; j < p.nb; ++j) {
+        BatchDesc &d = p.b[j];
+        d.ntiles = (uint32_t)((d.nbytes + T - 1) / T);
+        d.sbase = sb;
+        sb += d.ntiles;
+        d.cls = xl ? (j + 7u * p.nb) % 8u : 0u;   // (nb + cls) % 8 == j % 8
+        d.tile0 = cls_tiles[d.cls];
+        cls_tiles[d.cls] += d.ntiles;
+    }
+    if (sb > ds.max_tiles) return -EINVAL;
+    uint32_t grid_tiles = cls_tiles[0];
+    if (xl) {
+        uint32_t mx = 0;
+        for (int c = 0; c < 8; ++c) mx = cls_tiles[c] > mx ? cls_tiles[c] : mx;
+        grid_tiles = 8 * mx;
+    }
+    p.total_blocks = p.nb + grid_tiles;   // scanners first, then the tiles
     if (ds.wide() && hipMemsetAsync(&ds.d_ctl->pending, 0, sizeof(uint32_t), stream) != hipSuccess) return -EIO;
     hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     if (hipGetLastError() != hipSuccess) return -EIO;

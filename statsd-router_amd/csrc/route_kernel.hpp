@@ -46,9 +46,9 @@
 
 namespace srk {
 
-constexpr int kBlock = 512;                  // threads per workgroup of the product kernel (8 waves)
+constexpr int kBlock = 256;                  // threads per workgroup of the product kernel (4 waves)
 constexpr int kLaneBytes = 64;               // bytes per lane
-constexpr int kTile = kBlock * kLaneBytes;   // 32 KiB per tile
+constexpr int kTile = kBlock * kLaneBytes;   // 16 KiB per tile
 constexpr int kOverlay = 16;                 // register overlay entries of the probe
 constexpr int kNone = 0x1FFFF;               // "no colon" marker (above any tile position)
 constexpr int kSpinBudget = 1 << 14;         // polls before a missing predecessor is proxied
@@ -66,6 +66,7 @@ enum : unsigned {
     ABL_NO_SCAN = 8u,       // skip masks/Horner/scans (counts only)
     ABL_LOAD_ONLY = 16u,    // load the tile into LDS and count '\n' only
     ABL_STAMPS = 32u,       // diagnostic: s_memrealtime at phase boundaries into RouteParams::dbg
+    ABL_NO_XCD_LOCAL = 64u, // deal every launch's tiles round-robin even when it has 8+ batches
 };
 
 constexpr uint64_t ipow(uint64_t b, unsigned e) {
@@ -122,13 +123,16 @@ struct BatchDesc {
     uint64_t *n_out;         // device: line count of the batch
     uint32_t nbytes;
     uint32_t max_records;
-    uint32_t tile0;
+    uint32_t tile0;          // first tile in its XCD class's sequence (class 0 only: the launch's)
     uint32_t ntiles;
+    uint32_t sbase;          // first status / base granule of the batch
+    uint32_t cls;            // XCD class: the tiles of the batch are blocks nb + cls + 8 i
 };
 
 struct RouteParams {
     uint32_t nb;             // batches in this launch
-    uint32_t total_blocks;   // grid size: nb scanners + every batch's tiles
+    uint32_t total_blocks;   // grid size: nb scanners + every batch's tiles (+ padding blocks)
+    uint32_t xcd_local;      // 1: tile blocks dealt to 8 XCD classes, each batch within one class
     uint32_t nds;            // number of downstreams
     uint32_t dead;           // dead downstreams in the alive snapshot
     uint32_t pending_cap;
@@ -506,13 +510,13 @@ __device__ __forceinline__ bool granule_ok(uint64_t st, uint32_t ep, uint32_t fl
 template <int BLOCK>
 __device__ void scan_batch(const RouteParams &p, const BatchDesc &bd, uint32_t epoch, int lane) {
     constexpr int kGroups = 4;   // 64-tile groups polled per round
-    const uint64_t *status = p.status + bd.tile0;
-    uint64_t *bases = p.bases + bd.tile0;
+    const uint64_t *status = p.status + bd.sbase;
+    uint64_t *bases = p.bases + bd.sbase;
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
     const uint32_t ep = epoch & 0x3FFFFFFFu;
     uint32_t run = 0;
-    uint32_t c = 0;      // first tile whose base is not yet published (multiple of 64)
+    uint32_t c = 0;      // first tile whose base is not yet published
     int spin = 0;        // rounds without progress on group c
     while (c < bd.ntiles) {
         // one round trip: the counts of up to kGroups groups from c on
@@ -544,20 +548,23 @@ __device__ void scan_batch(const RouteParams &p, const BatchDesc &bd, uint32_t e
                 }
             }
         }
-        // publish the complete groups in order
+        // publish the longest complete prefix (tile by tile, so a tile never waits for a later one)
         bool progress = false;
 #pragma unroll
         for (int k = 0; k < kGroups; ++k) {
-            if (__ballot(!have[k])) break;
-            const uint32_t tt = c + lane;   // c has advanced by 64 per published group
-            const uint32_t incl = wave_incl_add32(cnt[k]);
-            if (tt < bd.ntiles)
-                __hip_atomic_store(&bases[tt], mk_status(epoch, kFlagBase, run + incl - cnt[k]), __ATOMIC_RELAXED,
+            const uint64_t missing = __ballot(!have[k]);
+            const int nready = missing ? __builtin_ctzll(missing) : 64;
+            if (nready == 0) break;
+            const uint32_t tt = c + lane;   // c has advanced by 64 per fully published group
+            const uint32_t v = lane < nready ? cnt[k] : 0u;
+            const uint32_t incl = wave_incl_add32(v);
+            if (lane < nready && tt < bd.ntiles)
+                __hip_atomic_store(&bases[tt], mk_status(epoch, kFlagBase, run + incl - v), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-            c += 64;
+            c += (uint32_t)nready;
             progress = true;
-            if (c >= bd.ntiles) break;
+            if (nready < 64 || c >= bd.ntiles) break;
         }
         if (progress) {
             spin = 0;
@@ -630,17 +637,26 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
         if (tid == 0) arrive(p, blockIdx.x, ep0);
         return;
     }
-    const uint32_t g = blockIdx.x - p.nb;   // tile index within the launch
-    // the batch of this tile (uniform; at most kMaxBatches scalar compares)
-    uint32_t bi = 0;
-    for (uint32_t k = 1; k < p.nb; ++k)
-        if (g >= p.b[k].tile0) bi = k;
+    const uint32_t g = blockIdx.x - p.nb;   // tile block index within the launch
+    // Launches of 8+ batches keep every batch on one XCD class (blocks b and b + 8 share an XCD):
+    // a tile's predecessors then start before it on the same dispatcher, and its scanner (block
+    // b, same class) sits beside them. The batch of this block: at most kMaxBatches scalar compares.
+    const uint32_t cls = p.xcd_local ? (g & 7u) : 0u;
+    const uint32_t ci = p.xcd_local ? (g >> 3) : g;
+    uint32_t bi = kMaxBatches;
+    for (uint32_t k = 0; k < p.nb; ++k)
+        if (p.b[k].cls == cls && ci >= p.b[k].tile0 && ci < p.b[k].tile0 + p.b[k].ntiles) bi = k;
+    if (bi == kMaxBatches) {   // padding block of an unbalanced class
+        const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0) arrive(p, blockIdx.x, ep0);
+        return;
+    }
     const BatchDesc &bd = p.b[bi];
     const uint8_t *const bytes = bd.bytes;
     const uint32_t nbytes = bd.nbytes, ntiles = bd.ntiles;
-    uint64_t *const status = p.status + bd.tile0;
-    const uint64_t *const base_slot = p.bases + bd.tile0 + (g - bd.tile0);
-    const uint32_t t = g - bd.tile0;   // tile index within the batch
+    const uint32_t t = ci - bd.tile0;   // tile index within the batch
+    uint64_t *const status = p.status + bd.sbase;
+    const uint64_t *const base_slot = p.bases + bd.sbase + t;
     const int64_t T0 = (int64_t)t * kTileB;
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)bytes, (short)0, (int)nbytes, 0x00020000);
@@ -724,7 +740,6 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
     // empty range (lane 0): count 0, no '\n', no colon
     const uint64_t eseg = seg_combine(sm.wave_pre[wave], wave_shr1_64(sseg, (uint64_t)kNone));
 
-    if (tid == 0) stamp<ABL>(p, tid, g, 3);
     // ---- last wave: where the line that straddles into the tile starts, its first ':' ----------
     if (wave == kPreWave) {
         int64_t s_abs = 0;
@@ -843,7 +858,9 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
                     else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
                     else route = probe_shard(h, p);                                                    // :145
                     if (!have_base) {   // needed only now, after the hash: normally long published
+                        stamp<ABL>(p, tid, g, 3);
                         base = wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
+                        stamp<ABL>(p, tid, g, 7);
                         have_base = true;
                     }
                     const uint32_t rec = base + (uint32_t)j;

@@ -109,13 +109,19 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
         const double u = 0.01;
         ph[0].push_back((d[1] - d[0]) * u);
         ph[1].push_back((d[2] - d[1]) * u);
-        ph[2].push_back((d[3] - d[2]) * u);
+        ph[2].push_back((d[7] - d[3]) * u);   // base wait (tid 0, first record)
         ph[3].push_back((d[4] - d[2]) * u);
         ph[4].push_back((d[5] - d[4]) * u);
         ph[5].push_back((d[6] - d[0]) * u);
     }
+    {
+        std::vector<double> w = ph[2];
+        std::sort(w.begin(), w.end());
+        printf("{\"base_wait_us_percentiles\": {\"p10\": %.2f, \"p50\": %.2f, \"p90\": %.2f, \"p99\": %.2f}}\n",
+               w[w.size() / 10], w[w.size() / 2], w[w.size() * 9 / 10], w[w.size() * 99 / 100]);
+    }
     printf("{\"mode\": \"%d batches per launch\", \"block\": %d, \"line_len\": %u, \"tiles\": %u, \"span_us\": %.2f, "
-           "\"median_us\": {\"load\": %.2f, \"masks_scan\": %.2f, \"lookback\": %.2f, \"to_staged\": %.2f, "
+           "\"median_us\": {\"load\": %.2f, \"masks_scan\": %.2f, \"base_wait\": %.2f, \"to_staged\": %.2f, "
            "\"hash_records\": %.2f, \"lifetime\": %.2f}}\n",
            L, BLOCK, line_len, total, (e1 - s0) * 0.01, med(ph[0]), med(ph[1]), med(ph[2]), med(ph[3]), med(ph[4]),
            med(ph[5]));
