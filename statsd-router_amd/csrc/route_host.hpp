@@ -54,6 +54,7 @@ struct DeviceState {
     uint64_t *d_alive = nullptr;
     Magic *d_magic = nullptr;
     uint64_t *d_kpow = nullptr;
+    uint4 *d_afrag = nullptr;
     Control *d_ctl = nullptr;
     uint64_t *d_status = nullptr;
     uint64_t *d_bases = nullptr;
@@ -95,6 +96,27 @@ struct DeviceState {
         }
         if (hipMemcpy(d_kpow, kp.data(), kp.size() * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess)
             return -EIO;
+        // int8 MFMA A fragments (route_kernel.hpp, hash_group): lane l, row r = l & 15, quarter
+        // q = l >> 4, byte j -> signed base-256 digit (r & 3) [+4 for the second table] of K^-(16q+j)
+        {
+            int8_t dig[64][8];
+            for (int pp = 0; pp < 64; ++pp) {
+                uint64_t w = ipow(kKinv, (unsigned)pp);
+                for (int r = 0; r < 8; ++r) {
+                    int d = (int)(w & 0xFF);
+                    if (d >= 128) d -= 256;
+                    dig[pp][r] = (int8_t)d;
+                    w = (w - (uint64_t)(int64_t)d) >> 8;
+                }
+            }
+            std::vector<int8_t> af(2 * 64 * 16);
+            for (int t = 0; t < 2; ++t)
+                for (int l = 0; l < 64; ++l)
+                    for (int j = 0; j < 16; ++j)
+                        af[(t * 64 + l) * 16 + j] = dig[16 * (l >> 4) + j][4 * t + ((l & 15) & 3)];
+            if (hipMalloc(&d_afrag, af.size()) != hipSuccess) return -ENOMEM;
+            if (hipMemcpy(d_afrag, af.data(), af.size(), hipMemcpyHostToDevice) != hipSuccess) return -EIO;
+        }
         for (uint32_t i = 0; i < n_downstreams; ++i) h_alive[i >> 6] |= 1ull << (i & 63);
         if (hipMemcpy(d_alive, h_alive, (nwords ? nwords : 1) * sizeof(uint64_t), hipMemcpyHostToDevice) !=
             hipSuccess)
@@ -107,6 +129,7 @@ struct DeviceState {
         (void)hipFree(d_alive);
         (void)hipFree(d_magic);
         (void)hipFree(d_kpow);
+        (void)hipFree(d_afrag);
         (void)hipFree(d_ctl);
         (void)hipFree(d_status);
         (void)hipFree(d_bases);
@@ -115,6 +138,7 @@ struct DeviceState {
         d_alive = nullptr;
         d_magic = nullptr;
         d_kpow = nullptr;
+        d_afrag = nullptr;
         d_ctl = nullptr;
         d_status = nullptr;
         d_bases = nullptr;
@@ -157,6 +181,7 @@ struct DeviceState {
         p.alive = d_alive;
         p.magic = d_magic;
         p.kpow = d_kpow;
+        p.afrag = d_afrag;
         p.ctl = d_ctl;
         p.status = d_status;
         p.bases = d_bases;

@@ -67,6 +67,7 @@ enum : unsigned {
     ABL_LOAD_ONLY = 16u,    // load the tile into LDS and count '\n' only
     ABL_STAMPS = 32u,       // diagnostic: s_memrealtime at phase boundaries into RouteParams::dbg
     ABL_NO_XCD_LOCAL = 64u, // deal every launch's tiles round-robin even when it has 8+ batches
+    ABL_MFMA_HASH = 128u,   // experiment: name hash as int8 MFMA digit sums (bit-exact, slower: DESIGN.md §6)
 };
 
 constexpr uint64_t ipow(uint64_t b, unsigned e) {
@@ -140,6 +141,7 @@ struct RouteParams {
     const uint64_t *alive;   // bitmap
     const Magic *magic;      // [0..nds], index i -> divisor i
     const uint64_t *kpow;    // kPowTable entries: K^i, K^(64 i), K^-i (i < 64)
+    const uint4 *afrag;      // [2][64]: per lane, the int8 MFMA A fragment of limbs 0-3 / 4-7 (hash_group)
     Control *ctl;
     uint64_t *status;        // per-tile '\n' count granules {epoch, flag, count} (written by the tile)
     uint64_t *bases;         // per-tile first-record granules {epoch, flag, base} (written by the scanner)
@@ -424,6 +426,7 @@ struct SmemT {
     uint64_t kp_lo[64];              // K^i
     uint64_t kp_hi[64];              // K^(64 i)
     uint64_t kinv[64];               // K^-i
+    uint32_t kmask[17][4];           // kmask[n]: 16-byte mask keeping the first n bytes
     int32_t s_pre, c_pre;            // straddling line: tile-relative start / first colon before T0
     uint32_t epoch, base;
 };
@@ -592,6 +595,76 @@ __device__ uint32_t wait_base(const uint64_t *slot, uint32_t epoch, __amdgpu_buf
     return n;
 }
 
+// ---- name hash on the matrix cores -----------------------------------------------------------
+// For a 64-byte segment of a name starting at byte a (name bytes c_0 .. c_{n-1}), with
+// W_p = K^-p mod 2^64 written in signed base-256 digits W_p = sum_r d_r(p) 256^r (d in [-128, 127]):
+//     T = sum_p c_p W_p = sum_r 256^r C_r,   C_r = sum_p c_p d_r(p)   (exact int32, |C_r| < 2^21)
+// and the sdbm of the whole name is  h = sum_k K^(n-1-64k) T_k  (mod 2^64) over its segments k.
+// One v_mfma_i32_16x16x64_i8 computes C_r for 16 segments (B columns = segments, 16 bytes per
+// lane, A rows = digits). A wave hashes 64 lines at a time: MFMA m takes the lines 16m .. 16m+15
+// with its digits in A rows 4m .. 4m+3, so its results land in rows 4m .. 4m+3 = lanes 16m .. 16m+15
+// (column = lane & 15): after the four MFMAs of a limb half, lane l holds the digit sums of line l.
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+
+template <class S>
+__device__ __forceinline__ v4i_t gather16(const S &sm, int a, int keep) {
+    // image bytes [a, a + 16), only the first `keep` (0..16) kept, as the MFMA's 16 int8
+    v4i_t out = {0, 0, 0, 0};
+    if (keep > 0) {
+        const int base = a & ~3, sh = a & 3;
+        const int i0 = img_dw(base), r0 = base & 63;
+        uint32_t w[5];
+#pragma unroll
+        for (int m = 0; m < 5; ++m) w[m] = sm.img[i0 + m + ((r0 + 4 * m) >> 6)];
+        const uint32_t *mk = sm.kmask[keep];
+#pragma unroll
+        for (int d = 0; d < 4; ++d) out[d] = (int)(__builtin_amdgcn_alignbyte(w[d + 1], w[d], sh) & mk[d]);
+    }
+    return out;
+}
+
+// Hash of the 64 lines of a wave: lane l's line starts at image byte a_l and has n_l name bytes
+// (0: no hash). Returns lane l's h.
+template <class S>
+__device__ __forceinline__ uint64_t hash_group(const S &sm, const uint4 *afrag, int a_me, int n_me, int lane) {
+    const int q = lane >> 4, col = lane & 15, rowgrp = col >> 2;
+    int kmax = (n_me + 63) >> 6;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) kmax = max(kmax, __shfl_xor(kmax, d, 64));
+    const v4i_t z = {0, 0, 0, 0};
+    const uint4 f1 = afrag[lane], f2 = afrag[64 + lane];
+    uint64_t h = 0;
+    for (int k = 0; k < kmax; ++k) {
+        v4i_t lo = z, hi = z;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            // the line of MFMA m this lane feeds (16m + col), its bytes [64k + 16q, +16)
+            const int am = __shfl(a_me, 16 * m + col, 64), nm = __shfl(n_me, 16 * m + col, 64);
+            const int off = 64 * k + 16 * q;
+            const int keep = min(max(nm - off, 0), 16);
+            const v4i_t b = gather16(sm, am + off, keep);
+            // this lane's A rows carry digits only in MFMA m == its row group (the select is
+            // re-done per MFMA: an opaque copy keeps the compiler from holding 8 fragments)
+            uint4 g1 = f1, g2 = f2;
+            asm volatile("" : "+v"(g1.x), "+v"(g1.y), "+v"(g1.z), "+v"(g1.w));
+            asm volatile("" : "+v"(g2.x), "+v"(g2.y), "+v"(g2.z), "+v"(g2.w));
+            const bool on = rowgrp == m;
+            const v4i_t F1 = {on ? (int)g1.x : 0, on ? (int)g1.y : 0, on ? (int)g1.z : 0, on ? (int)g1.w : 0};
+            const v4i_t F2 = {on ? (int)g2.x : 0, on ? (int)g2.y : 0, on ? (int)g2.z : 0, on ? (int)g2.w : 0};
+            lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(F1, b, lo, 0, 0, 0);
+            hi = __builtin_amdgcn_mfma_i32_16x16x64_i8(F2, b, hi, 0, 0, 0);
+        }
+        if (n_me > 64 * k) {
+            const int32_t p01 = lo[0] + (lo[1] << 8), p23 = lo[2] + (lo[3] << 8);
+            const int32_t p45 = hi[0] + (hi[1] << 8), p67 = hi[2] + (hi[3] << 8);
+            const uint64_t T = (uint64_t)(int64_t)p01 + ((uint64_t)(int64_t)p23 << 16) +
+                               ((uint64_t)((uint32_t)p45 + ((uint32_t)p67 << 16)) << 32);
+            h += T * kpow_n(sm, n_me - 1 - 64 * k);
+        }
+    }
+    return h;
+}
+
 // Arrivals: every block adds itself to a sharded counter (no return value, nothing waits); the
 // last block waits until all have arrived, then resets the counters and advances the epoch.
 // Every block read the epoch before arriving, so none of this launch can see the new one.
@@ -664,6 +737,10 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
     stamp<ABL>(p, tid, g, 0);
     if (tid == 0) sm.epoch = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < kPowTable) (&sm.kp_lo[0])[tid] = p.kpow[tid];   // kp_lo | kp_hi | kinv are contiguous
+    if (tid < 68) {   // kmask[n][d]: bytes 4d .. 4d+3 of a mask keeping the first n bytes
+        const int n = tid >> 2, d = tid & 3, kb = min(max(n - 4 * d, 0), 4);
+        sm.kmask[n][d] = kb == 4 ? 0xFFFFFFFFu : ((1u << (8 * kb)) - 1u);
+    }
     if (tid < kHalo / 16) {   // the 2 KiB before the tile (zeros before the batch start)
         uint4 hv = make_uint4(0, 0, 0, 0);
         if (t > 0 && !(ABL & ABL_NO_PROLOGUE))
@@ -824,7 +901,54 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
         }
         __syncthreads();
         if (wbase == 0) stamp<ABL>(p, tid, g, 4);
-        if (!(ABL & ABL_NO_LINES)) {
+        if ((ABL & ABL_MFMA_HASH) && !(ABL & ABL_NO_LINES)) {
+            // 64 lines per wave at a time; lane l owns line grp*64 + l (hash on the matrix cores)
+            const int s_pre = sm.s_pre;
+            const int c_pre = sm.c_pre;
+            const int nwin = min(kWin, (int)tile_count - wbase);
+            for (int grp = wave; grp * 64 < nwin; grp += kWaves) {
+                const int jj = grp * 64 + lane;
+                const bool mine = jj < nwin;
+                const int j = wbase + jj;
+                int s = 0, e = 0, c = kNone;
+                if (mine) {
+                    e = sm.lend[jj + 1];
+                    c = sm.lcol[jj + 1];
+                    if (j == 0 && c_pre != kNone) c = c_pre;   // the straddling line's ':' lies before T0
+                    s = (j == 0) ? s_pre : sm.lend[jj] + 1;
+                }
+                const int len = e - s + 1;
+                const bool len_ok = len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH;   // :180
+                const bool fmt_ok = c != kNone && c < e;                                                // :140
+                const int n = (mine && len_ok && fmt_ok) ? c - s : 0;
+                const uint64_t h = hash_group(sm, p.afrag, kHalo + s, n, lane);
+                if (mine) {
+                    uint32_t route;
+                    if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
+                    else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
+                    else route = probe_shard(h, p);                                                    // :145
+                    if (!have_base) {   // needed only now, after the hash: normally long published
+                        stamp<ABL>(p, tid, g, 3);
+                        base = wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
+                        stamp<ABL>(p, tid, g, 7);
+                        have_base = true;
+                    }
+                    const uint32_t rec = base + (uint32_t)j;
+                    if (rec < bd.max_records) {
+                        if (route == kRoutePending) {
+                            const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
+                            if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
+                        }
+                        sr_record r;
+                        r.offset = (uint32_t)(T0 + s);
+                        r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
+                        r.route = (uint16_t)route;
+                        bd.recs[rec] = r;
+                        if (bd.hashes) bd.hashes[rec] = h;
+                    }
+                }
+            }
+        } else if (!(ABL & ABL_NO_LINES)) {
             const int s_pre = sm.s_pre;
             const int c_pre = sm.c_pre;
             const int nwin = min(kWin, (int)tile_count - wbase);
