@@ -113,7 +113,7 @@ int sr_route_device(sr_ctx *ctx, const uint8_t *d_bytes, size_t nbytes, sr_recor
  * routed together, each exactly as sr_route_device would route it alone. Up to
  * SR_MAX_BATCHES_PER_LAUNCH batches share a kernel launch; larger counts are split into several
  * launches. Each batch must fit max_batch_bytes. Returns 0 or -EINVAL / -EIO. */
-#define SR_MAX_BATCHES_PER_LAUNCH 16u
+#define SR_MAX_BATCHES_PER_LAUNCH 32u
 typedef struct sr_batch {
     const uint8_t *d_bytes;  /* framed datagrams, device memory                         */
     size_t nbytes;

@@ -55,7 +55,7 @@ SR_MAX_OWNERS = 64
 def pack_capacity(nbytes: int) -> int:
     """SR_PACK_CAPACITY: packed-bytes room that always suffices for a batch of nbytes."""
     return nbytes + nbytes // 2 + 4
-SR_MAX_BATCHES_PER_LAUNCH = 16
+SR_MAX_BATCHES_PER_LAUNCH = 32
 
 
 class SrBatch(ctypes.Structure):

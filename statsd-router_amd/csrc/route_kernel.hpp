@@ -116,7 +116,7 @@ struct Control {
 // One batch of a launch. A launch routes up to kMaxBatches independent batches: tiles
 // [tile0, tile0 + ntiles) of the grid belong to batch i, each batch with its own look-back chain
 // (status granules at the same grid indices) and its own records and line count.
-constexpr int kMaxBatches = 16;
+constexpr int kMaxBatches = 32;
 struct BatchDesc {
     const uint8_t *bytes;
     sr_record *recs;

@@ -62,7 +62,7 @@ size_t sr_frame_datagrams(uint8_t *dst, size_t dst_cap, const uint8_t *const *dg
 }
 
 const char *sr_version(void) {
-    return "statsd-router-mi355x 0.5 (gfx950 route_kernel: 16 KiB tiles x 256 threads, per-batch scanners, up to 16 batches per launch)";
+    return "statsd-router-mi355x 0.5 (gfx950 route_kernel: 16 KiB tiles x 256 threads, per-batch scanners, up to 32 batches per launch)";
 }
 
 void sr_close(sr_ctx *c) {
