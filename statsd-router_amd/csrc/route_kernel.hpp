@@ -67,6 +67,7 @@ enum : unsigned {
     ABL_LOAD_ONLY = 16u,    // load the tile into LDS and count '\n' only
     ABL_STAMPS = 32u,       // diagnostic: s_memrealtime at phase boundaries into RouteParams::dbg
     ABL_NO_XCD_LOCAL = 64u, // deal every launch's tiles round-robin even when it has 8+ batches
+    ABL_NO_HASH = 256u,     // ablation: skip the sdbm (h = 0); staging, probe and records stay
     ABL_MFMA_HASH = 128u,   // experiment: name hash as int8 MFMA digit sums (bit-exact, slower: DESIGN.md §6)
 };
 
@@ -967,7 +968,7 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
                 const bool len_ok = len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH;   // :180
                 const bool fmt_ok = c != kNone && c < e;                                                // :140
                 uint64_t h = 0;
-                if (len_ok && fmt_ok) {
+                if (len_ok && fmt_ok && !(ABL & ABL_NO_HASH)) {
                     // sdbm of [s, c) = sum over 64-byte segments k of Horner(seg_k) * K^(c - end_k)
                     const int n = c - s, nseg = (n + 63) >> 6;
                     for (int k = gi; k < nseg; k += G) {

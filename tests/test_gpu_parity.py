@@ -247,3 +247,25 @@ def test_device_many_batches_one_launch(pkg, oracle, dead):
             recs = d_out[i].cpu().numpy().view(pkg.RECORD_DTYPE)[:k]
             hs = d_h[i].cpu().numpy().view(np.uint64)[:k]
             _assert_same((recs, hs, k), oracle.route(p, n, alive), f"batch {i}")
+
+
+def test_device_many_splits_past_launch_limit(pkg, oracle):
+    """More batches than one launch takes (SR_MAX_BATCHES_PER_LAUNCH): split into launches."""
+    import torch
+
+    n = pkg.SR_MAX_BATCHES_PER_LAUNCH + 9
+    parts = [pkg.gen_stream(20_000 + 3_001 * i, [64, 256], seed=400 + i, p_invalid=0.05).data for i in range(n)]
+    with pkg.Router(7, 1 << 20) as r:
+        r.set_stream(torch.cuda.current_stream().cuda_stream)
+        d_in = [torch.from_numpy(p.copy()).to("cuda") for p in parts]
+        d_out = [torch.empty(int(p.size) * 8, dtype=torch.uint8, device="cuda") for p in parts]
+        d_n = torch.full((n,), -1, dtype=torch.int64, device="cuda")
+        r.route_device_many([(d_in[i].data_ptr(), int(p.size), d_out[i].data_ptr(), int(p.size), None,
+                              d_n.data_ptr() + 8 * i) for i, p in enumerate(parts)])
+        torch.cuda.synchronize()
+        counts = d_n.cpu().numpy()
+        for i, p in enumerate(parts):
+            k = int(counts[i])
+            recs = d_out[i].cpu().numpy().view(pkg.RECORD_DTYPE)[:k]
+            exp, _, en = oracle.route(p, 7)
+            assert k == en and np.array_equal(recs, exp), f"batch {i}"

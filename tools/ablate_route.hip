@@ -147,9 +147,8 @@ int main(int argc, char **argv) {
             rows[i++].us[round] = us;
         };
         put("b512_m16", time_variant<512, ABL_NONE>(c, 1, reps, 16));
-        put("b256_m32", time_variant<256, ABL_NONE>(c, 1, reps, 32));
-        put("b512_m32", time_variant<512, ABL_NONE>(c, 1, reps, 32));
-        put("b256_m32_no_xcd_local", time_variant<256, ABL_NO_XCD_LOCAL>(c, 1, reps, 32));
+        put("b256_m16_no_hash", time_variant<256, ABL_NO_HASH>(c, 1, reps, 16));
+        put("b512_m16_no_hash", time_variant<512, ABL_NO_HASH>(c, 1, reps, 16));
         put("b256_m16_mfma_hash", time_variant<256, ABL_MFMA_HASH>(c, 1, reps, 16));
         put("b1024_m16", time_variant<1024, ABL_NONE>(c, 1, reps, 16));
         put("b256_m16", time_variant<256, ABL_NONE>(c, 1, reps, 16));
