@@ -262,7 +262,30 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
         for (int c = 0; c < 8; ++c) mx = cls_tiles[c] > mx ? cls_tiles[c] : mx;
         grid_tiles = 8 * mx;
     }
+    for (int c = 0; c < 8; ++c) p.cls_tiles[c] = cls_tiles[c];
+    if (ABL & ABL_PAIR) {   // one workgroup per two tiles of a class
+        uint32_t mx = 0;
+        for (int c = 0; c < (xl ? 8 : 1); ++c) mx = (cls_tiles[c] + 1) / 2 > mx ? (cls_tiles[c] + 1) / 2 : mx;
+        grid_tiles = xl ? 8 * mx : mx;
+    }
     p.total_blocks = p.nb + grid_tiles;   // scanners first, then the tiles
+    if (ABL & ABL_PERSIST) {
+        // as many tile workgroups as stay resident beside the scanners, dealt evenly to the classes
+        static int slots = 0;
+        if (!slots) {
+            int occ = 0, dev = 0, cus = 0;
+            if (hipGetDevice(&dev) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, route_kernel<BLOCK, ABL>, BLOCK, 0) != hipSuccess)
+                return -EIO;
+            slots = occ * cus;
+        }
+        uint32_t nwg = (uint32_t)slots > p.nb + 8 ? (uint32_t)slots - p.nb : 8u;
+        if (xl) nwg &= ~7u;
+        if (nwg > grid_tiles) nwg = grid_tiles;
+        p.nwg = nwg;
+        p.total_blocks = p.nb + nwg;
+    }
     if (ds.wide() && hipMemsetAsync(&ds.d_ctl->pending, 0, sizeof(uint32_t), stream) != hipSuccess) return -EIO;
     hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     if (hipGetLastError() != hipSuccess) return -EIO;

@@ -52,6 +52,7 @@ constexpr int kTile = kBlock * kLaneBytes;   // 16 KiB per tile
 constexpr int kOverlay = 16;                 // register overlay entries of the probe
 constexpr int kNone = 0x1FFFF;               // "no colon" marker (above any tile position)
 constexpr int kSpinBudget = 1 << 14;         // polls before a missing predecessor is proxied
+constexpr int kLookRounds = 1;               // look-back reach: 64 tiles per round
 constexpr uint32_t kFlagAgg = 1u, kFlagIncl = 2u;
 constexpr uint16_t kRoutePending = 0xFFFCu;  // internal: resolved by probe_wide_kernel
 constexpr uint64_t K = 65599ull;             // sdbm multiplier: (h<<6)+(h<<16)-h (sr-main.c:131)
@@ -69,6 +70,14 @@ enum : unsigned {
     ABL_NO_XCD_LOCAL = 64u, // deal every launch's tiles round-robin even when it has 8+ batches
     ABL_NO_HASH = 256u,     // ablation: skip the sdbm (h = 0); staging, probe and records stay
     ABL_MFMA_HASH = 128u,   // experiment: name hash as int8 MFMA digit sums (bit-exact, slower: DESIGN.md §6)
+    ABL_PERSIST = 512u,     // persistent tile workgroups: each loops over tiles, loading tile i+1 while routing tile i
+    ABL_OLD_MASKS = 65536u,  // round-1 v0.5 piece masks (one SWAR test per pattern)
+    ABL_OLD_SCANNER = 32768u, // round-1 v0.5 scanner: one wave polls and publishes
+    ABL_DEFER = 16384u,     // the last window's records kept in LDS; base by look-back, then written
+    ABL_PAIR = 8192u,       // two tiles per workgroup: the second's loads and count up front, the first's records late
+    ABL_FAKE_BASE = 4096u,  // ablation: base = t * (this tile's count), exact only for uniform tiles (C2)
+    ABL_LATE_BASE = 2048u,  // read the record base only after hashing (round-1 v0.5)
+    ABL_OLD_HASH = 1024u,   // round-1 v0.5 per-segment sdbm (v_alignbyte reads, compiler-extracted bytes)
 };
 
 constexpr uint64_t ipow(uint64_t b, unsigned e) {
@@ -112,6 +121,7 @@ struct Control {
     uint32_t pending;
     uint32_t pad0[29];
     uint32_t done[8][32];
+    uint32_t grab[8][32];   // ABL_PERSIST: next tile of each XCD class (handed out in order)
 };
 
 // One batch of a launch. A launch routes up to kMaxBatches independent batches: tiles
@@ -148,6 +158,8 @@ struct RouteParams {
     uint64_t *bases;         // per-tile first-record granules {epoch, flag, base} (written by the scanner)
     PendingLine *pending;
     uint64_t *dbg;           // ABL_STAMPS builds only: 8 timestamps per tile
+    uint32_t nwg;            // ABL_PERSIST: tile workgroups of the launch (a multiple of 8 when xcd_local)
+    uint32_t cls_tiles[8];   // tiles per XCD class (class 0 only without xcd_local)
     BatchDesc b[kMaxBatches];
 };
 
@@ -170,6 +182,33 @@ __device__ __forceinline__ uint64_t sdbm_dword(uint64_t h, uint32_t x) {
     const int32_t t = c0 * (int32_t)K + c1;
     const int32_t u = c2 * (int32_t)K + c3;
     const uint64_t d = (uint64_t)((int64_t)t * kK2lo) + (uint64_t)(int64_t)u + ((uint64_t)(uint32_t)t << 32);
+    return h * kK4 + d;
+}
+
+// Signed-byte pair products by SDWA (byte select + sign extension folded into the VALU op):
+// c0 * K + c1 and c2 * K + c3 for the bytes c0..c3 of x, two instructions each.
+__device__ __forceinline__ int32_t pair_lo(uint32_t x) {
+    int32_t t;
+    asm("v_mul_i32_i24_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD\n\t"
+        "v_add_u32_sdwa %0, %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+        : "=&v"(t)
+        : "v"(x), "v"((int32_t)K));
+    return t;
+}
+__device__ __forceinline__ int32_t pair_hi(uint32_t x) {
+    int32_t t;
+    asm("v_mul_i32_i24_sdwa %0, sext(%1), %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD\n\t"
+        "v_add_u32_sdwa %0, %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+        : "=&v"(t)
+        : "v"(x), "v"((int32_t)K));
+    return t;
+}
+
+// sdbm_dword with the pair products from SDWA: 11 VALU per dword.
+__device__ __forceinline__ uint64_t sdbm_dword_fast(uint64_t h, uint32_t x) {
+    const int32_t t = pair_lo(x);
+    const int32_t u = pair_hi(x);
+    const uint64_t d = (uint64_t)((int64_t)t * kK2lo + (int64_t)u) + ((uint64_t)(uint32_t)t << 32);
     return h * kK4 + d;
 }
 
@@ -215,6 +254,44 @@ __device__ __forceinline__ uint32_t eq_mask16_dot(uint4 v, uint32_t pat) {
     uint32_t hi = __builtin_amdgcn_udot4(eq_flags(v.z, pat), 0x08040201u, 0u, false);
     hi = __builtin_amdgcn_udot4(eq_flags(v.w, pat), 0x80402010u, hi, false);
     return (lo + (hi << 8)) >> 7;
+}
+
+// '\n' and ':' masks (bit i = byte i) of a 16-byte piece, 8 VALU per dword for both patterns.
+// For a pattern P with bit 7 clear, byte b == P iff bit 7 of b is clear and ((b & 0x7F) ^ P) + 0x7F
+// has bit 7 clear (the sum stays within the byte): the masked bytes and ~b's bit 7 are shared by
+// both patterns, the xor-add is one v_xad_u32, and the flag one v_bfi_b32.
+__device__ __forceinline__ uint32_t not_and(uint32_t a, uint32_t b) {   // ~a & b
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, 0, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t xor_add(uint32_t a, uint32_t x, uint32_t y) {   // (a ^ x) + y
+    uint32_t r;
+    asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(x), "v"(y));
+    return r;
+}
+__device__ __forceinline__ uint32_t nl_colon_mask16(uint4 v) {   // '\n' mask | ':' mask << 16
+    const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+    uint32_t an = 0, cn = 0, ah = 0, ch = 0;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+        const uint32_t x = xs[d];
+        const uint32_t x7 = x & 0x7F7F7F7Fu;
+        const uint32_t nx = not_and(x, 0x80808080u);
+        const uint32_t fn = not_and(xor_add(x7, 0x0A0A0A0Au, 0x7F7F7F7Fu), nx);
+        const uint32_t fc = not_and(xor_add(x7, 0x3A3A3A3Au, 0x7F7F7F7Fu), nx);
+        const uint32_t w = (d & 1) ? 0x80402010u : 0x08040201u;
+        if (d < 2) {
+            an = __builtin_amdgcn_udot4(fn, w, an, false);
+            cn = __builtin_amdgcn_udot4(fc, w, cn, false);
+        } else {
+            ah = __builtin_amdgcn_udot4(fn, w, ah, false);
+            ch = __builtin_amdgcn_udot4(fc, w, ch, false);
+        }
+    }
+    const uint32_t nl = (an + (ah << 8)) >> 7;
+    const uint32_t cl = (cn + (ch << 8)) >> 7;
+    return nl | (cl << 16);
 }
 
 // number of bytes equal to the replicated pattern
@@ -306,6 +383,7 @@ __device__ __forceinline__ uint64_t wave_scan64(uint64_t v, uint64_t id, F f) {
 
 // value of the lane below (lane 0: id)
 __device__ __forceinline__ uint64_t wave_shr1_64(uint64_t v, uint64_t id) { return dpp64<kDppWaveShr1>(id, v); }
+__device__ __forceinline__ uint32_t wave_shr1_32(uint32_t v, uint32_t id) { return dpp32<kDppWaveShr1>(id, v); }
 
 __device__ __forceinline__ uint32_t wave_add32(uint32_t v) {   // sum over the wave, in every lane
     v += dpp32<kDppRowShr1>(0u, v);
@@ -325,6 +403,26 @@ __device__ __forceinline__ uint32_t wave_incl_add32(uint32_t v) {
     v += dpp32<kDppRowShr8>(0u, v);
     v += dpp32<kDppRowBcast15, 0xA>(0u, v);
     v += dpp32<kDppRowBcast31, 0xC>(0u, v);
+    return v;
+}
+
+// inclusive wave64 max / min scans of a u32 (DPP)
+__device__ __forceinline__ uint32_t wave_incl_max32(uint32_t v) {
+    v = max(v, dpp32<kDppRowShr1>(0u, v));
+    v = max(v, dpp32<kDppRowShr2>(0u, v));
+    v = max(v, dpp32<kDppRowShr4>(0u, v));
+    v = max(v, dpp32<kDppRowShr8>(0u, v));
+    v = max(v, dpp32<kDppRowBcast15, 0xA>(0u, v));
+    v = max(v, dpp32<kDppRowBcast31, 0xC>(0u, v));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_incl_min32(uint32_t v) {
+    v = min(v, dpp32<kDppRowShr1>(0xFFFFFFFFu, v));
+    v = min(v, dpp32<kDppRowShr2>(0xFFFFFFFFu, v));
+    v = min(v, dpp32<kDppRowShr4>(0xFFFFFFFFu, v));
+    v = min(v, dpp32<kDppRowShr8>(0xFFFFFFFFu, v));
+    v = min(v, dpp32<kDppRowBcast15, 0xA>(0xFFFFFFFFu, v));
+    v = min(v, dpp32<kDppRowBcast31, 0xC>(0xFFFFFFFFu, v));
     return v;
 }
 
@@ -406,7 +504,7 @@ struct SmemT {
     static constexpr int kWaves = BLOCK / 64;
     static constexpr int kTileB = BLOCK * kLaneBytes;
     static constexpr int kHalo = 2048;                // bytes before the tile kept in LDS
-    static constexpr int kWin = 2 * BLOCK;            // tile-local lines staged per round
+    static constexpr int kWin = BLOCK;                // tile-local lines staged per round
     // LDS image of the batch bytes [T0 - kHalo, T0 + tile): 64-byte rows stored as 17 dwords (one
     // pad dword per row) so that lanes reading at 64-byte strides hit distinct banks.
     static constexpr int kRows = (kHalo + kTileB) / 64;
@@ -419,17 +517,22 @@ struct SmemT {
         struct {
             int32_t lend[kWin + 1];  // per staged line: tile position of its '\n'; slot 0 = previous
             int32_t lcol[kWin + 1];  // per staged line: first ':' in the tile part (kNone if none)
+            sr_record rec[kWin];     // the last window's records, written once the base is known
         };
     };
     uint64_t wave_seg[kWaves];
     uint64_t wave_pre[kWaves];       // exclusive line state of each wave
     uint32_t wave_cnt[kWaves];
+    uint32_t wave_cnt2[kWaves];      // pair mode: the second tile's per-wave '\n' counts
+    uint32_t wave_scan[kWaves][4];   // per wave, inclusive at its last lane: '\n' count, latest '\n' lane, colon key
     uint64_t kp_lo[64];              // K^i
     uint64_t kp_hi[64];              // K^(64 i)
     uint64_t kinv[64];               // K^-i
     uint32_t kmask[17][4];           // kmask[n]: 16-byte mask keeping the first n bytes
     int32_t s_pre, c_pre;            // straddling line: tile-relative start / first colon before T0
     uint32_t epoch, base;
+    uint32_t grab, grab0;            // ABL_PERSIST: tile indices handed to this workgroup
+    uint32_t scan_head, scan_pub, scan_total;   // scanner: bases computed / published, line total
 };
 
 // K^n for 0 <= n < 4096 from the LDS tables
@@ -465,6 +568,26 @@ __device__ __forceinline__ uint64_t sdbm_lds(const S &sm, int a, int n) {
         x &= (1u << (8 * rem)) - 1u;
         h = sdbm_dword(h, x) * sm.kinv[4 - rem];
     }
+    return h;
+}
+
+// sdbm of the 0 < n <= 64 image bytes starting at image byte a, from aligned dword reads: the
+// bytes of the first dword before a are zeroed (leading zeros leave a Horner value unchanged), the
+// last partial dword is zero-padded and the padding undone by K^-z. Dword m of the run is p[m]
+// before the row's pad dword and p[m + 1] after it.
+template <class S>
+__device__ __forceinline__ uint64_t sdbm_img(const S &sm, int a, int n) {
+    const int lead = a & 3, L = lead + n;
+    const int F = L >> 2, rem = L & 3;
+    const int dw = a >> 2, s16 = dw & 15, cross = 16 - s16;
+    const uint32_t *const p = &sm.img[(dw >> 4) * 17 + s16];
+    const uint32_t first = p[0] & (0xFFFFFFFFu << (8 * lead));
+    if (F == 0) return sdbm_dword_fast(0, first & ((1u << (8 * rem)) - 1u)) * sm.kinv[4 - rem];
+    uint64_t h = sdbm_dword_fast(0, first);
+    int m = 1;
+    for (; m < F && m < cross; ++m) h = sdbm_dword_fast(h, p[m]);
+    for (; m < F; ++m) h = sdbm_dword_fast(h, p[m + 1]);
+    if (rem) h = sdbm_dword_fast(h, p[m + (m >= cross ? 1 : 0)] & ((1u << (8 * rem)) - 1u)) * sm.kinv[4 - rem];
     return h;
 }
 
@@ -580,6 +703,101 @@ __device__ void scan_batch(const RouteParams &p, const BatchDesc &bd, uint32_t e
     if (lane == 0) *bd.n_out = run;
 }
 
+// Scanner with its global stores split off (the product's): on gfx9 a wave's stores share vmcnt
+// with its loads, so a scanner that also published would wait for its own stores before every
+// poll. Wave 0 polls the tiles' counts and computes their bases into an LDS ring (head index
+// released after the writes); wave 1 publishes the ring to the bases granules and the batch's
+// line count. Flow control keeps the ring (the LDS image, 4096 entries) from overrunning.
+template <int BLOCK>
+__device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint32_t epoch, SmemT<BLOCK> &sm,
+                                 int wave, int lane) {
+    constexpr uint32_t kRing = 4096;
+    static_assert(SmemT<BLOCK>::kWords >= (int)kRing, "scanner ring in the LDS image");
+    uint32_t *const ring = sm.img;
+    if (wave == 0) {
+        constexpr int kGroups = 4;
+        const uint64_t *status = p.status + bd.sbase;
+        const __amdgpu_buffer_rsrc_t rsrc =
+            __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
+        const uint32_t ep = epoch & 0x3FFFFFFFu;
+        uint32_t run = 0, c = 0;
+        int spin = 0;
+        while (c < bd.ntiles) {
+            // the publisher must have taken the ring slots this round may overwrite
+            while (c + 64 * kGroups > __hip_atomic_load(&sm.scan_pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) +
+                                          kRing)
+                __builtin_amdgcn_s_sleep(1);
+            uint32_t cnt[kGroups];
+            bool have[kGroups];
+#pragma unroll
+            for (int k = 0; k < kGroups; ++k) {
+                const uint32_t tt = c + 64 * k + lane;
+                cnt[k] = 0;
+                have[k] = tt >= bd.ntiles;
+                if (!have[k]) {
+                    const uint64_t st = __hip_atomic_load(&status[tt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (granule_ok(st, ep, kFlagAgg)) {
+                        cnt[k] = (uint32_t)st;
+                        have[k] = true;
+                    }
+                }
+            }
+            if (spin >= kSpinBudget) {   // head group still incomplete: count its silent tiles here
+                uint64_t missing = __ballot(!have[0]);
+                while (missing) {
+                    const int L = __builtin_ctzll(missing);
+                    missing &= missing - 1;
+                    const uint32_t c2 = count_tile_wave<BLOCK>(bd.nbytes, rsrc, c + (uint32_t)L, lane);
+                    if (lane == L) {
+                        cnt[0] = c2;
+                        have[0] = true;
+                    }
+                }
+            }
+            const uint32_t c_start = c;
+#pragma unroll
+            for (int k = 0; k < kGroups; ++k) {
+                const uint64_t missing = __ballot(!have[k]);
+                const int nready = missing ? __builtin_ctzll(missing) : 64;
+                if (nready == 0) break;
+                const uint32_t v = lane < nready ? cnt[k] : 0u;
+                const uint32_t incl = wave_incl_add32(v);
+                if (lane < nready && c + lane < bd.ntiles) ring[(c + lane) % kRing] = run + incl - v;
+                run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                c += (uint32_t)nready;
+                if (nready < 64 || c >= bd.ntiles) break;
+            }
+            if (c > bd.ntiles) c = bd.ntiles;
+            if (c != c_start) {
+                spin = 0;
+                if (lane == 0) {
+                    if (c >= bd.ntiles) sm.scan_total = run;
+                    __hip_atomic_store(&sm.scan_head, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            } else {
+                ++spin;
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    } else if (wave == 1) {
+        uint64_t *const bases = p.bases + bd.sbase;
+        uint32_t pub = 0;
+        while (pub < bd.ntiles) {
+            const uint32_t h = __hip_atomic_load(&sm.scan_head, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (h == pub) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            for (uint32_t i = pub + lane; i < h; i += 64)
+                __hip_atomic_store(&bases[i], mk_status(epoch, kFlagBase, ring[i % kRing]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            pub = h;
+            if (lane == 0) __hip_atomic_store(&sm.scan_pub, pub, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if (lane == 0) *bd.n_out = __hip_atomic_load(&sm.scan_total, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
 // a tile's first record index, from its scanner (per lane; the lanes of a wave read one address).
 // Fallback after a long wait (never taken when blocks are dispatched in order): count the '\n'
 // bytes before the tile directly.
@@ -681,105 +899,131 @@ __device__ void arrive(const RouteParams &p, uint32_t blk, uint32_t epoch) {
         __builtin_amdgcn_s_sleep(2);
     }
 #pragma unroll
-    for (int s8 = 0; s8 < 8; ++s8)
+    for (int s8 = 0; s8 < 8; ++s8) {
         __hip_atomic_store(&p.ctl->done[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&p.ctl->grab[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     __hip_atomic_store(&p.ctl->epoch, epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int BLOCK>
+template <int BLOCK, unsigned ABL>
 struct KernelTraits {
     // waves per SIMD to reserve registers for: 1024-thread tiles run one workgroup per CU,
-    // smaller tiles several (LDS: 86 KB / 45 KB / 24 KB per workgroup)
-    static constexpr int kMinWavesPerSimd = BLOCK >= 1024 ? 4 : 6;
+    // smaller tiles several (LDS: 86 KB / 45 KB / 24 KB per workgroup); persistent workgroups
+    // hold a second tile in registers and hide latency by prefetch instead of occupancy
+    static constexpr int kMinWavesPerSimd = (ABL & ABL_PERSIST) ? 4 : (ABL & ABL_PAIR) ? 5 : (BLOCK >= 1024 ? 4 : 6);
+    static constexpr int kMaxWavesPerSimd = (ABL & ABL_PERSIST) ? 4 : (ABL & ABL_PAIR) ? 5 : 8;
+};
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, never for its
+// outstanding global loads (a persistent workgroup keeps the next tile's loads in flight across it).
+__device__ __forceinline__ void wg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// The batch of tile ci of XCD class cls (kMaxBatches if none): at most kMaxBatches scalar compares.
+__device__ __forceinline__ uint32_t batch_of(const RouteParams &p, uint32_t cls, uint32_t ci) {
+    uint32_t bi = kMaxBatches;
+    for (uint32_t k = 0; k < p.nb; ++k)
+        if (p.b[k].cls == cls && ci >= p.b[k].tile0 && ci < p.b[k].tile0 + p.b[k].ntiles) bi = k;
+    return bi;
+}
+
+// One tile's input as loaded into registers: piece P = k*BLOCK + tid of the tile (bytes 16P ..) in
+// v[k]; threads below kHalo/16 also hold 16 bytes of the 2 KiB before the tile.
+struct TileIn {
+    uint32_t bi, t;
+    uint4 v[4];
+    uint4 hv;
 };
 
 template <int BLOCK, unsigned ABL>
-__global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void route_kernel(RouteParams p) {
+__device__ __forceinline__ void tile_issue(const RouteParams &p, uint32_t bi, uint32_t t, TileIn &in, int tid) {
+    constexpr int kTileB = BLOCK * kLaneBytes;
+    constexpr int kHalo = SmemT<BLOCK>::kHalo;
+    const BatchDesc &bd = p.b[bi];
+    const uint32_t T0 = t * (uint32_t)kTileB;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
+    in.bi = bi;
+    in.t = t;
+    in.hv = make_uint4(0, 0, 0, 0);
+    if (tid < kHalo / 16 && t > 0 && !(ABL & ABL_NO_PROLOGUE))   // zeros before the batch start
+        in.hv = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, T0 - kHalo + tid * 16, 0, 0));
+#pragma unroll
+    for (int k = 0; k < 4; ++k) in.v[k] = load16(rsrc, T0 + k * BLOCK * 16 + tid * 16, bd.nbytes);
+}
+
+// Route one tile (reference: sr-main.c:175-189 + process_data_line + hash + find_downstream's
+// choice, for every line that ends in the tile), in two halves. First half: the tile's bytes from
+// the registers of `in` into the LDS image, the '\n' / ':' masks of every piece, and the tile's
+// '\n' count published for the scanner. Needs the LDS free of the previous tile's readers.
+template <int BLOCK, unsigned ABL>
+__device__ __forceinline__ void tile_load_lds(const RouteParams &p, SmemT<BLOCK> &sm, const TileIn &in, uint32_t epoch,
+                                              uint32_t g) {
+    using S = SmemT<BLOCK>;
+    constexpr int kWaves = S::kWaves;
+    constexpr int kHalo = S::kHalo;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    uint64_t *const status = p.status + p.b[in.bi].sbase;
+
+    stamp<ABL>(p, tid, g, 0);
+    if (tid < kHalo / 16) img_put16(sm, tid * 16, in.hv);
+    // the '\n' / ':' masks of each piece are taken from the registers (-> sm.pm) and the '\n' count
+    // with them, so the tile's aggregate can be published early
+    {
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            img_put16(sm, kHalo + 16 * (k * BLOCK + tid), in.v[k]);
+            uint32_t m;
+            if (ABL & ABL_OLD_MASKS) m = eq_mask16_dot(in.v[k], 0x0A0A0A0Au) | (eq_mask16_dot(in.v[k], 0x3A3A3A3Au) << 16);
+            else m = nl_colon_mask16(in.v[k]);
+            sm.pm[k * BLOCK + tid] = m;
+            cnt += __popc(m & 0xFFFFu);
+        }
+        cnt = wave_add32(cnt);
+        if (lane == 0) sm.wave_cnt[wave] = cnt;
+    }
+    wg_barrier();
+    stamp<ABL>(p, tid, g, 1);
+    uint32_t tile_count = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) tile_count += sm.wave_cnt[w];
+    if (tid == 0) {   // publish this tile's '\n' count for the scanner
+        const uint64_t st = mk_status(epoch, kFlagAgg, tile_count);
+        __hip_atomic_store(&status[in.t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Second half: lines, hashes, shards and records of the tile whose bytes tile_load_lds left in the
+// LDS. Ends with every LDS reader done (the next tile may overwrite the image).
+template <int BLOCK, unsigned ABL>
+__device__ __forceinline__ uint2 tile_lines(const RouteParams &p, SmemT<BLOCK> &sm, const TileIn &in, uint32_t epoch,
+                                            uint32_t g, sr_record *defer = nullptr) {
+    uint2 deferred = make_uint2(0u, 0u);   // {first tile-local line, lines} of the records left in `defer`
+    stamp<ABL>(p, threadIdx.x, g, 1);
     using S = SmemT<BLOCK>;
     constexpr int kWaves = S::kWaves;
     constexpr int kTileB = S::kTileB;
     constexpr int kHalo = S::kHalo;
     constexpr int kWin = S::kWin;
     constexpr int kPreWave = kWaves - 1;   // the wave that locates the straddling line
-    __shared__ S sm;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    if (blockIdx.x < p.nb) {   // scanner of batch blockIdx.x (wave 0; no barriers on this path)
-        const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (wave == 0) scan_batch<BLOCK>(p, p.b[blockIdx.x], ep0, lane);
-        if (tid == 0) arrive(p, blockIdx.x, ep0);
-        return;
-    }
-    const uint32_t g = blockIdx.x - p.nb;   // tile block index within the launch
-    // Launches of 8+ batches keep every batch on one XCD class (blocks b and b + 8 share an XCD):
-    // a tile's predecessors then start before it on the same dispatcher, and its scanner (block
-    // b, same class) sits beside them. The batch of this block: at most kMaxBatches scalar compares.
-    const uint32_t cls = p.xcd_local ? (g & 7u) : 0u;
-    const uint32_t ci = p.xcd_local ? (g >> 3) : g;
-    uint32_t bi = kMaxBatches;
-    for (uint32_t k = 0; k < p.nb; ++k)
-        if (p.b[k].cls == cls && ci >= p.b[k].tile0 && ci < p.b[k].tile0 + p.b[k].ntiles) bi = k;
-    if (bi == kMaxBatches) {   // padding block of an unbalanced class
-        const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (tid == 0) arrive(p, blockIdx.x, ep0);
-        return;
-    }
+    const uint32_t bi = in.bi, t = in.t;
     const BatchDesc &bd = p.b[bi];
-    const uint8_t *const bytes = bd.bytes;
-    const uint32_t nbytes = bd.nbytes, ntiles = bd.ntiles;
-    const uint32_t t = ci - bd.tile0;   // tile index within the batch
-    uint64_t *const status = p.status + bd.sbase;
+    const uint32_t nbytes = bd.nbytes;
     const uint64_t *const base_slot = p.bases + bd.sbase + t;
     const int64_t T0 = (int64_t)t * kTileB;
     const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)bytes, (short)0, (int)nbytes, 0x00020000);
-
-    stamp<ABL>(p, tid, g, 0);
-    if (tid == 0) sm.epoch = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (tid < kPowTable) (&sm.kp_lo[0])[tid] = p.kpow[tid];   // kp_lo | kp_hi | kinv are contiguous
-    if (tid < 68) {   // kmask[n][d]: bytes 4d .. 4d+3 of a mask keeping the first n bytes
-        const int n = tid >> 2, d = tid & 3, kb = min(max(n - 4 * d, 0), 4);
-        sm.kmask[n][d] = kb == 4 ? 0xFFFFFFFFu : ((1u << (8 * kb)) - 1u);
-    }
-    if (tid < kHalo / 16) {   // the 2 KiB before the tile (zeros before the batch start)
-        uint4 hv = make_uint4(0, 0, 0, 0);
-        if (t > 0 && !(ABL & ABL_NO_PROLOGUE))
-            hv = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)(T0 - kHalo) + tid * 16, 0, 0));
-        img_put16(sm, tid * 16, hv);
-    }
-    if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
-    // coalesced tile load: wave instruction k of thread tid covers piece P = k*BLOCK + tid (bytes
-    // 16P ..); the '\n' / ':' masks of the piece are taken from the registers (-> sm.pm) and the
-    // '\n' count with them, so the tile's aggregate can be published early
-    {
-        uint4 v[4];
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = load16(rsrc, (uint32_t)T0 + k * BLOCK * 16 + tid * 16, nbytes);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            img_put16(sm, kHalo + 16 * (k * BLOCK + tid), v[k]);
-            const uint32_t nl = eq_mask16_dot(v[k], 0x0A0A0A0Au);
-            const uint32_t cl = eq_mask16_dot(v[k], 0x3A3A3A3Au);
-            sm.pm[k * BLOCK + tid] = nl | (cl << 16);
-            cnt += __popc(nl);
-        }
-        cnt = wave_add32(cnt);
-        if (lane == 0) sm.wave_cnt[wave] = cnt;
-    }
-    __syncthreads();
-    stamp<ABL>(p, tid, g, 1);
-    const uint32_t epoch = sm.epoch;
+        __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)nbytes, 0x00020000);
     uint32_t tile_count = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) tile_count += sm.wave_cnt[w];
-    if (tid == 0) {   // publish this tile's '\n' count for the scanner
-        const uint64_t st = mk_status(epoch, kFlagAgg, tile_count);
-        __hip_atomic_store(&status[t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
     if (ABL & ABL_LOAD_ONLY) {
-        __syncthreads();
+        wg_barrier();
     } else {
     // ---- per lane: '\n' / ':' masks of its 64 contiguous bytes, segmented line-state scan -------
     const int o = tid * kLaneBytes;   // tile position of the lane's first byte
@@ -795,34 +1039,68 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
         clm = ((uint64_t)c_hi << 32) | c_lo;
     }
     const int ncnt = __popcll(nlm);
-    uint64_t seg;
-    if (nlm) {
-        const int lastb = 63 - __clzll(nlm);
-        const uint64_t after = lastb == 63 ? 0ull : (clm & (~0ull << (lastb + 1)));
-        const uint32_t fc = after ? (uint32_t)(o + __builtin_ctzll(after)) : (uint32_t)kNone;
-        seg = ((uint64_t)ncnt << 32) | 0x80000000u | fc;
-    } else {
-        seg = clm ? (uint32_t)(o + __builtin_ctzll(clm)) : (uint32_t)kNone;
+    // Line state before each lane's chunk, by three u32 wave scans (DPP) and a prefix over the
+    // earlier waves: the number of '\n' before it, and the first ':' of the line open at its start.
+    //  * the colon candidate of a chunk is its first ':' after its last '\n' (or its first ':' if it
+    //    holds no '\n'): the first ':' of the line open at a chunk's end is the smallest candidate
+    //    from the latest chunk with a '\n' on;
+    //  * key = ((BLOCK - L) << 17) | candidate, L = 1 + latest thread with a '\n' up to here (0: none
+    //    in this wave), so a min-scan of keys takes the smallest candidate of the latest segment.
+    uint32_t cand;
+    {
+        uint64_t cm = clm;
+        if (nlm) {
+            const int lastb = 63 - __clzll(nlm);
+            cm = lastb == 63 ? 0ull : (clm & (~0ull << (lastb + 1)));
+        }
+        cand = cm ? (uint32_t)(o + __builtin_ctzll(cm)) : (uint32_t)kNone;
     }
-    auto comb = [](uint64_t f, uint64_t g) { return seg_combine(f, g); };
-    const uint64_t sseg = wave_scan64(seg, (uint64_t)kNone, comb);
-    if (lane == 63) sm.wave_seg[wave] = sseg;
-    __syncthreads();
+    const uint32_t c_in = wave_incl_add32((uint32_t)ncnt);
+    const uint32_t l_in = wave_incl_max32(nlm ? (uint32_t)tid + 1u : 0u);
+    const uint32_t k_in = wave_incl_min32(((uint32_t)(BLOCK - (int)l_in) << 17) | cand);
+    if (lane == 63) *(uint4 *)&sm.wave_scan[wave][0] = make_uint4(c_in, l_in, k_in, 0u);
+    wg_barrier();
     stamp<ABL>(p, tid, g, 2);
-    if (wave == 0) {   // exclusive line state of every wave
-        const uint64_t v = wave_scan64(lane < kWaves ? sm.wave_seg[lane] : (uint64_t)kNone, (uint64_t)kNone, comb);
-        const uint64_t ex = wave_shr1_64(v, (uint64_t)kNone);
-        if (lane < kWaves) sm.wave_pre[lane] = ex;
+    uint32_t p_cnt = 0, p_col = (uint32_t)kNone;   // the earlier waves: '\n' count, open line's first ':'
+#pragma unroll
+    for (int w = 0; w < kWaves - 1; ++w) {
+        if (w < wave) {
+            const uint4 ws = *(const uint4 *)&sm.wave_scan[w][0];
+            p_cnt += ws.x;
+            const uint32_t wc = ws.z & 0x1FFFFu;
+            p_col = ws.y ? wc : min(p_col, wc);
+        }
     }
-    __syncthreads();
-    // empty range (lane 0): count 0, no '\n', no colon
-    const uint64_t eseg = seg_combine(sm.wave_pre[wave], wave_shr1_64(sseg, (uint64_t)kNone));
+    // exclusive state of this lane: the inclusive state of the lane below, on top of the prefix
+    const uint32_t c_ex = wave_shr1_32(c_in, 0u);
+    const uint32_t l_ex = wave_shr1_32(l_in, 0u);
+    const uint32_t k_ex = wave_shr1_32(k_in, 0xFFFFFFFFu) & 0x1FFFFu;
+    const int lane_first = (int)(p_cnt + c_ex);                       // tile-local index of lane's 1st line
+    const int open_fc = (int)(l_ex ? k_ex : min(p_col, k_ex));        // first ':' (in the tile) of the open line
 
     // ---- last wave: where the line that straddles into the tile starts, its first ':' ----------
     if (wave == kPreWave) {
         int64_t s_abs = 0;
         int32_t c_pre = kNone;
-        if (t > 0 && !(ABL & ABL_NO_PROLOGUE)) {
+        // fast window: the last 512 bytes before the tile, 8 per lane (a line of up to 512 bytes)
+        const int fb = kHalo - 512 + 8 * lane;
+        const uint32_t y0 = sm.img[img_dw(fb)], y1 = sm.img[img_dw(fb + 4)];
+        const uint32_t nl8 = eq_mask4(y0, 0x0A0A0A0Au) | (eq_mask4(y1, 0x0A0A0A0Au) << 4);
+        const uint64_t fm = __ballot(nl8 != 0);
+        if (t > 0 && !(ABL & ABL_NO_PROLOGUE) && fm) {
+            const int L = 63 - __builtin_clzll(fm);
+            const int pos = (int)__builtin_amdgcn_readlane(fb + 31 - __builtin_clz(nl8 | 1u), L);
+            s_abs = T0 - kHalo + pos + 1;
+            // the line's first ':' before T0 lies in the window too
+            const int b0 = pos + 1 - fb;   // first byte of the line within my 8
+            const uint32_t keep = b0 <= 0 ? 0xFFu : (b0 >= 8 ? 0u : (0xFFu & ~((1u << b0) - 1u)));
+            const uint32_t cm8 = (eq_mask4(y0, 0x3A3A3A3Au) | (eq_mask4(y1, 0x3A3A3A3Au) << 4)) & keep;
+            const uint64_t cb = __ballot(cm8 != 0);
+            if (cb) {
+                const int Lc = __builtin_ctzll(cb);
+                c_pre = (int)__builtin_amdgcn_readlane(fb + __builtin_ctz(cm8 | 0x100u), Lc) - kHalo;
+            }
+        } else if (t > 0 && !(ABL & ABL_NO_PROLOGUE)) {
             // the halo: lane l looks at LDS bytes [32l, 32l + 32) = positions T0 - 2048 + 32l ...
             const uint4 a0 = img_get16(sm, 32 * lane), a1 = img_get16(sm, 32 * lane + 16);
             const uint32_t nl32 = eq_mask16(a0, 0x0A0A0A0Au) | (eq_mask16(a1, 0x0A0A0A0Au) << 16);
@@ -869,11 +1147,9 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
     }
 
     // ---- per line: windows of kWin tile-local lines ------------------------------------------
-    const int lane_first = (int)(eseg >> 32);               // tile-local index of lane's 1st line
-    const int open_fc = (int)((uint32_t)eseg & 0x1FFFFu);   // first ':' (in the tile) of the open line
     if (tid == 0) sm.lend[0] = 0;
-    uint32_t base = 0;                                        // first record index of the tile
-    bool have_base = (ABL & (ABL_NO_LOOKBACK | ABL_NO_LINES)) != 0;
+    uint32_t base = (ABL & ABL_FAKE_BASE) ? t * tile_count : 0u;   // first record index of the tile
+    bool have_base = (ABL & (ABL_NO_LOOKBACK | ABL_NO_LINES | ABL_FAKE_BASE)) != 0;
     for (int wbase = 0; wbase < (int)tile_count; wbase += kWin) {
         // (1) stage (e, c) of the lane's lines that fall into this window
         if (nlm && lane_first + ncnt > wbase && lane_first < wbase + kWin) {
@@ -900,8 +1176,31 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
                 prevb = b;
             }
         }
-        __syncthreads();
+        wg_barrier();
         if (wbase == 0) stamp<ABL>(p, tid, g, 4);
+        // the tile's record base, read ahead: the load's round trip overlaps the hashing, and the
+        // granule is re-polled at record time only if the scanner had not yet published it
+        uint64_t st_early = 0;
+        if (!have_base && !(ABL & ABL_LATE_BASE))
+            st_early = __hip_atomic_load(base_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // Deferred records (the tile's last window): the records are kept in LDS and written after
+        // the window loop, once wave 0 has the base. Wave 0 reads ahead the granules of the kLook
+        // tiles before this one (lane i, round r: tile t-1-64r-i), for a look-back that does not wait
+        // for the scanner: base(t) = base(j) + counts of j .. t-1, j the nearest tile whose base is
+        // published (by the scanner or by a tile's own look-back) with every count in between.
+        const bool defer_tile = (ABL & ABL_DEFER) && !have_base && wbase + kWin >= (int)tile_count && !bd.hashes &&
+                                p.dead <= (uint32_t)kOverlay;
+        uint64_t lb_cnt[kLookRounds], lb_base[kLookRounds];
+#pragma unroll
+        for (int r = 0; r < kLookRounds; ++r) {
+            lb_cnt[r] = 0;
+            lb_base[r] = 0;
+            const int jt = (int)t - 1 - 64 * r - lane;
+            if (defer_tile && wave == 0 && jt >= 0) {
+                lb_cnt[r] = __hip_atomic_load(p.status + bd.sbase + jt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                lb_base[r] = __hip_atomic_load(p.bases + bd.sbase + jt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
         if ((ABL & ABL_MFMA_HASH) && !(ABL & ABL_NO_LINES)) {
             // 64 lines per wave at a time; lane l owns line grp*64 + l (hash on the matrix cores)
             const int s_pre = sm.s_pre;
@@ -930,7 +1229,9 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
                     else route = probe_shard(h, p);                                                    // :145
                     if (!have_base) {   // needed only now, after the hash: normally long published
                         stamp<ABL>(p, tid, g, 3);
-                        base = wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
+                        base = granule_ok(st_early, epoch & 0x3FFFFFFFu, kFlagBase)
+                                   ? (uint32_t)st_early
+                                   : wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
                         stamp<ABL>(p, tid, g, 7);
                         have_base = true;
                     }
@@ -953,66 +1254,298 @@ __global__ __launch_bounds__(BLOCK, KernelTraits<BLOCK>::kMinWavesPerSimd) void 
             const int s_pre = sm.s_pre;
             const int c_pre = sm.c_pre;
             const int nwin = min(kWin, (int)tile_count - wbase);
+            // the records of the tile's last window may be left in `defer` (no base wait here)
+            const bool defer_win = (defer != nullptr && wbase + kWin >= (int)tile_count) || defer_tile;
+            sr_record *const dbuf = defer != nullptr ? defer : sm.rec;
             // lanes per line from the mean line length: 64-byte hash segments per lane
             const int mean = kTileB / max((int)tile_count, 1);
             int G = 1;
             while (G < 32 && G * 64 < mean) G <<= 1;
             const int nG = BLOCK / G, gi = tid & (G - 1);
-            for (int jj = tid / G; jj < nwin; jj += nG) {
+            // wave-uniform rounds (the base resolution below needs every lane of the wave)
+            for (int jr = 0; jr < nwin; jr += nG) {
+                const int jj = jr + tid / G;
+                const bool act = jj < nwin;
                 const int j = wbase + jj;
-                const int e = sm.lend[jj + 1];
-                int c = sm.lcol[jj + 1];
+                const int e = act ? sm.lend[jj + 1] : 0;
+                int c = act ? sm.lcol[jj + 1] : kNone;
                 if (j == 0 && c_pre != kNone) c = c_pre;   // the straddling line's ':' lies before T0
-                const int s = (j == 0) ? s_pre : sm.lend[jj] + 1;
+                const int s = (j == 0) ? s_pre : (act ? sm.lend[jj] + 1 : 0);
                 const int len = e - s + 1;
                 const bool len_ok = len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH;   // :180
                 const bool fmt_ok = c != kNone && c < e;                                                // :140
                 uint64_t h = 0;
-                if (len_ok && fmt_ok && !(ABL & ABL_NO_HASH)) {
+                if (act && len_ok && fmt_ok && !(ABL & ABL_NO_HASH)) {
                     // sdbm of [s, c) = sum over 64-byte segments k of Horner(seg_k) * K^(c - end_k)
                     const int n = c - s, nseg = (n + 63) >> 6;
                     for (int k = gi; k < nseg; k += G) {
                         const int a = s + 64 * k, nn = min(64, n - 64 * k);
-                        h += sdbm_lds(sm, a + kHalo, nn) * kpow_n(sm, c - a - nn);
+                        uint64_t hs = (ABL & ABL_OLD_HASH) ? sdbm_lds(sm, a + kHalo, nn) : sdbm_img(sm, a + kHalo, nn);
+                        if (k + 1 < nseg) hs *= kpow_n(sm, c - a - nn);   // the last segment ends at c
+                        h += hs;
                     }
                 }
                 for (int d = G >> 1; d >= 1; d >>= 1) h += shfl_xor64(h, d);
-                if (gi == 0) {
+                if (act && gi == 0) {
                     uint32_t route;
                     if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
                     else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
                     else route = probe_shard(h, p);                                                    // :145
-                    if (!have_base) {   // needed only now, after the hash: normally long published
-                        stamp<ABL>(p, tid, g, 3);
-                        base = wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
-                        stamp<ABL>(p, tid, g, 7);
-                        have_base = true;
-                    }
-                    const uint32_t rec = base + (uint32_t)j;
-                    if (rec < bd.max_records) {
-                        if (route == kRoutePending) {
-                            const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
-                            if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
+                    sr_record r;
+                    r.offset = (uint32_t)(T0 + s);
+                    r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
+                    r.route = (uint16_t)route;
+                    if (defer_win) {   // the record base is read later
+                        dbuf[jj] = r;
+                    } else {
+                        if (!have_base) {   // needed only now, after the hash: normally long published
+                            stamp<ABL>(p, tid, g, 3);
+                            base = granule_ok(st_early, epoch & 0x3FFFFFFFu, kFlagBase)
+                                       ? (uint32_t)st_early
+                                       : wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
+                            stamp<ABL>(p, tid, g, 7);
+                            have_base = true;
                         }
-                        sr_record r;
-                        r.offset = (uint32_t)(T0 + s);
-                        r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
-                        r.route = (uint16_t)route;
-                        bd.recs[rec] = r;
-                        if (bd.hashes) bd.hashes[rec] = h;
+                        const uint32_t rec = base + (uint32_t)j;
+                        if (rec < bd.max_records) {
+                            if (route == kRoutePending) {
+                                const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
+                                if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
+                            }
+                            bd.recs[rec] = r;
+                            if (bd.hashes) bd.hashes[rec] = h;
+                        }
                     }
                 }
             }
+            if (defer_win) deferred = make_uint2((uint32_t)wbase, (uint32_t)nwin);
         }
-        __syncthreads();
+        if (defer_tile && deferred.y) {   // the window loop ends here
+            wg_barrier();   // every record of the window is in sm.rec
+            if (wave == 0) {
+                const uint32_t ep = epoch & 0x3FFFFFFFu;
+                uint32_t b = 0;
+                bool ok = granule_ok(st_early, ep, kFlagBase);
+                if (ok) b = (uint32_t)st_early;
+                uint32_t acc = 0;
+#pragma unroll
+                for (int r = 0; r < kLookRounds; ++r) {
+                    if (ok) break;
+                    const int jt = (int)t - 1 - 64 * r - lane;
+                    const bool okc = jt < 0 || granule_ok(lb_cnt[r], ep, kFlagAgg);
+                    const bool okb = jt == -1 || (jt >= 0 && granule_ok(lb_base[r], ep, kFlagBase));
+                    const uint64_t mc = __ballot(okc), mb = __ballot(okb);
+                    const uint64_t have = ~mc ? ((1ull << __builtin_ctzll(~mc)) - 1ull) : ~0ull;
+                    const uint64_t cands = mb & have;
+                    const uint32_t cv = jt >= 0 ? (uint32_t)lb_cnt[r] : 0u;
+                    if (cands) {
+                        const int i = __builtin_ctzll(cands);
+                        const uint32_t bj = jt >= 0 ? (uint32_t)lb_base[r] : 0u;
+                        b = (uint32_t)__builtin_amdgcn_readlane((int)bj, i) + acc + wave_add32(lane <= i ? cv : 0u);
+                        ok = true;
+                    } else if (~mc) {
+                        break;   // a count missing before any anchor
+                    } else {
+                        acc += wave_add32(cv);
+                    }
+                }
+                if (!ok) b = wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
+                if (lane == 0) {
+                    sm.base = b;
+                    // published for the look-backs of later tiles (the scanner writes the same value)
+                    __hip_atomic_store((uint64_t *)base_slot, mk_status(epoch, kFlagBase, b), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            wg_barrier();
+            const uint32_t b0 = sm.base + (uint32_t)wbase;
+            for (uint32_t i = (uint32_t)tid; i < deferred.y; i += BLOCK) {
+                const uint32_t rec = b0 + i;
+                if (rec < bd.max_records) bd.recs[rec] = sm.rec[i];
+            }
+            deferred = make_uint2(0u, 0u);
+        }
+        wg_barrier();
         if (wbase == 0) stamp<ABL>(p, tid, g, 5);
         if (tid == 0) sm.lend[0] = sm.lend[min(kWin, (int)tile_count - wbase)];
-        __syncthreads();
+        wg_barrier();
     }
     }
     stamp<ABL>(p, tid, g, 6);
+    return deferred;
+}
 
-    if (tid == 0) arrive(p, blockIdx.x, epoch);
+// Write the records tile_lines left in `buf` (after its closing barrier): the tile's record base
+// has been published by now in all but rare cases, so the poll normally succeeds at once.
+template <int BLOCK>
+__device__ __forceinline__ void flush_records(const RouteParams &p, const TileIn &in, const sr_record *buf, uint2 d,
+                                              uint32_t epoch) {
+    if (d.y == 0) return;
+    const BatchDesc &bd = p.b[in.bi];
+    const uint32_t T0 = in.t * (uint32_t)(BLOCK * kLaneBytes);
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
+    const uint32_t base = wait_base(p.bases + bd.sbase + in.t, epoch, rsrc, T0) + d.x;
+    for (uint32_t i = threadIdx.x; i < d.y; i += BLOCK) {
+        const uint32_t rec = base + i;
+        if (rec < bd.max_records) bd.recs[rec] = buf[i];
+    }
+}
+
+// Pair mode: the second tile's bytes stay in registers while the first is routed; its masks and
+// '\n' count are taken from the registers up front (count published early), then this writes its
+// LDS image and piece masks. Needs the LDS free of the first tile's readers.
+template <int BLOCK, unsigned ABL>
+__device__ __forceinline__ void tile_store_lds(SmemT<BLOCK> &sm, const TileIn &in, const uint32_t pm[4]) {
+    constexpr int kHalo = SmemT<BLOCK>::kHalo;
+    const int tid = threadIdx.x;
+    if (tid < kHalo / 16) img_put16(sm, tid * 16, in.hv);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        img_put16(sm, kHalo + 16 * (k * BLOCK + tid), in.v[k]);
+        sm.pm[k * BLOCK + tid] = pm[k];
+    }
+    if (tid < SmemT<BLOCK>::kWaves) sm.wave_cnt[tid] = sm.wave_cnt2[tid];
+    wg_barrier();
+}
+
+template <int BLOCK, unsigned ABL>
+__global__ __launch_bounds__(BLOCK, (KernelTraits<BLOCK, ABL>::kMinWavesPerSimd))
+__attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd), (KernelTraits<BLOCK, ABL>::kMaxWavesPerSimd)))) void route_kernel(RouteParams p) {
+    using S = SmemT<BLOCK>;
+    __shared__ S sm;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    if (blockIdx.x < p.nb) {   // scanner of batch blockIdx.x (wave 0; no barriers on this path)
+        const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ABL & ABL_OLD_SCANNER) {
+            if (wave == 0) scan_batch<BLOCK>(p, p.b[blockIdx.x], ep0, lane);
+            if (tid == 0) arrive(p, blockIdx.x, ep0);
+        } else {
+            if (tid == 0) {
+                sm.scan_head = 0;
+                sm.scan_pub = 0;
+                sm.scan_total = 0;
+            }
+            wg_barrier();
+            scan_batch_split<BLOCK>(p, p.b[blockIdx.x], ep0, sm, wave, lane);
+            if (tid == 64) arrive(p, blockIdx.x, ep0);   // the publisher, after its last store
+        }
+        return;
+    }
+    const uint32_t g = blockIdx.x - p.nb;   // tile workgroup index within the launch
+    // Launches of 8+ batches keep every batch on one XCD class (blocks b and b + 8 share an XCD):
+    // a tile's predecessors then start before it on the same dispatcher, and its scanner (block
+    // b, same class) sits beside them.
+    const uint32_t cls = p.xcd_local ? (g & 7u) : 0u;
+    uint32_t ci = p.xcd_local ? (g >> 3) : g;
+    const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ABL & ABL_PAIR) {   // tiles 2ci and 2ci + 1 of the class
+        __shared__ sr_record rec_buf[S::kWin];
+        const uint32_t c0 = 2 * ci, c1 = c0 + 1;
+        const uint32_t b0 = batch_of(p, cls, c0);
+        if (b0 == kMaxBatches) {
+            if (tid == 0) arrive(p, blockIdx.x, ep0);
+            return;
+        }
+        const uint32_t b1 = batch_of(p, cls, c1);
+        const bool has_b = b1 != kMaxBatches;
+        TileIn ta, tb;
+        tile_issue<BLOCK, ABL>(p, b0, c0 - p.b[b0].tile0, ta, tid);
+        if (has_b) tile_issue<BLOCK, ABL>(p, b1, c1 - p.b[b1].tile0, tb, tid);
+        if (tid < kPowTable) (&sm.kp_lo[0])[tid] = p.kpow[tid];
+        if (tid < 68) {
+            const int n = tid >> 2, d = tid & 3, kb = min(max(n - 4 * d, 0), 4);
+            sm.kmask[n][d] = kb == 4 ? 0xFFFFFFFFu : ((1u << (8 * kb)) - 1u);
+        }
+        if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
+        tile_load_lds<BLOCK, ABL>(p, sm, ta, ep0, g);
+        uint32_t pmb[4] = {0u, 0u, 0u, 0u};
+        if (has_b) {   // the second tile's masks and count from its registers; count published now
+            uint32_t cnt = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                pmb[k] = nl_colon_mask16(tb.v[k]);
+                cnt += __popc(pmb[k] & 0xFFFFu);
+            }
+            cnt = wave_add32(cnt);
+            if (lane == 0) sm.wave_cnt2[wave] = cnt;
+            wg_barrier();
+            if (tid == 0) {
+                uint32_t tc = 0;
+#pragma unroll
+                for (int w = 0; w < S::kWaves; ++w) tc += sm.wave_cnt2[w];
+                __hip_atomic_store(&p.status[p.b[b1].sbase + tb.t], mk_status(ep0, kFlagAgg, tc), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        const bool can_defer = has_b && !(ABL & ABL_MFMA_HASH) && !p.b[b0].hashes && p.dead <= (uint32_t)kOverlay;
+        const uint2 da = tile_lines<BLOCK, ABL>(p, sm, ta, ep0, g, can_defer ? rec_buf : nullptr);
+        if (has_b) tile_store_lds<BLOCK, ABL>(sm, tb, pmb);
+        flush_records<BLOCK>(p, ta, rec_buf, da, ep0);
+        if (has_b) tile_lines<BLOCK, ABL>(p, sm, tb, ep0, g);
+        if (tid == 0) arrive(p, blockIdx.x, ep0);
+        return;
+    }
+    if (!(ABL & ABL_PERSIST)) {   // one tile per workgroup
+        const uint32_t bi = batch_of(p, cls, ci);
+        if (bi == kMaxBatches) {   // padding block of an unbalanced class
+            if (tid == 0) arrive(p, blockIdx.x, ep0);
+            return;
+        }
+        TileIn in;
+        tile_issue<BLOCK, ABL>(p, bi, ci - p.b[bi].tile0, in, tid);
+        if (tid < kPowTable) (&sm.kp_lo[0])[tid] = p.kpow[tid];   // kp_lo | kp_hi | kinv are contiguous
+        if (tid < 68) {   // kmask[n][d]: bytes 4d .. 4d+3 of a mask keeping the first n bytes
+            const int n = tid >> 2, d = tid & 3, kb = min(max(n - 4 * d, 0), 4);
+            sm.kmask[n][d] = kb == 4 ? 0xFFFFFFFFu : ((1u << (8 * kb)) - 1u);
+        }
+        if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
+        tile_load_lds<BLOCK, ABL>(p, sm, in, ep0, g);
+        tile_lines<BLOCK, ABL>(p, sm, in, ep0, g);
+        if (tid == 0) arrive(p, blockIdx.x, ep0);
+        return;
+    }
+    // persistent: the workgroups of a class take its tiles in order from a shared counter (no
+    // rounds: a tile's predecessors were handed out before it). The next tile's loads are in flight
+    // while the current one's lines are routed, and its '\n' count is published straight after.
+    const uint32_t total = p.cls_tiles[cls];
+    uint32_t *const grab = &p.ctl->grab[cls][0];
+    if (tid < kPowTable) (&sm.kp_lo[0])[tid] = p.kpow[tid];
+    if (tid < 68) {
+        const int n = tid >> 2, d = tid & 3, kb = min(max(n - 4 * d, 0), 4);
+        sm.kmask[n][d] = kb == 4 ? 0xFFFFFFFFu : ((1u << (8 * kb)) - 1u);
+    }
+    if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
+    if (tid == 0) sm.grab0 = atomicAdd(grab, 1u);
+    wg_barrier();
+    ci = sm.grab0;
+    TileIn cur, nxt;
+    uint32_t cn = total;
+    if (ci < total) {
+        const uint32_t bi = batch_of(p, cls, ci);
+        tile_issue<BLOCK, ABL>(p, bi, ci - p.b[bi].tile0, cur, tid);
+        if (tid == 0) sm.grab = atomicAdd(grab, 1u);
+        tile_load_lds<BLOCK, ABL>(p, sm, cur, ep0, p.b[cur.bi].sbase + cur.t);   // barrier inside
+        cn = sm.grab;
+    }
+    while (ci < total) {
+        if (cn < total) {
+            const uint32_t bn = batch_of(p, cls, cn);
+            tile_issue<BLOCK, ABL>(p, bn, cn - p.b[bn].tile0, nxt, tid);
+        }
+        uint32_t cnn = 0;
+        if (tid == 0 && cn < total) cnn = atomicAdd(grab, 1u);   // the tile after next
+        tile_lines<BLOCK, ABL>(p, sm, cur, ep0, p.b[cur.bi].sbase + cur.t);
+        if (tid == 0) sm.grab = cn < total ? cnn : total;
+        wg_barrier();   // every reader of the current tile's LDS is done; sm.grab written
+        if (cn < total) tile_load_lds<BLOCK, ABL>(p, sm, nxt, ep0, p.b[nxt.bi].sbase + nxt.t);
+        cur = nxt;
+        ci = cn;
+        cn = sm.grab;
+    }
+    if (tid == 0) arrive(p, blockIdx.x, ep0);
 }
 
 // Lines whose probe met more than kOverlay dead shards: run find_downstream (sr-main.c:86-117)

@@ -146,17 +146,31 @@ int main(int argc, char **argv) {
             if (round == 0) rows.push_back(Row{name, {0, 0, 0}});
             rows[i++].us[round] = us;
         };
+        put("b256_m16_old_masks", time_variant<256, ABL_OLD_MASKS>(c, 1, reps, 16));
+        put("b256_m16_old_scanner", time_variant<256, ABL_OLD_SCANNER>(c, 1, reps, 16));
+        put("b256_m16_pair", time_variant<256, ABL_PAIR>(c, 1, reps, 16));
+        put("b256_m16_pair_fake_base", time_variant<256, ABL_PAIR | ABL_FAKE_BASE>(c, 1, reps, 16));
+        put("b256_m16_fake_base", time_variant<256, ABL_FAKE_BASE>(c, 1, reps, 16));
+        put("b256_m16_fake_base_no_hash", time_variant<256, ABL_FAKE_BASE | ABL_NO_HASH>(c, 1, reps, 16));
+        put("b256_m16_late_base", time_variant<256, ABL_LATE_BASE>(c, 1, reps, 16));
+        put("b256_m16_old_hash", time_variant<256, ABL_OLD_HASH>(c, 1, reps, 16));
+        put("b256_m16_old_hash_no_lookback", time_variant<256, ABL_OLD_HASH | ABL_NO_LOOKBACK>(c, 1, reps, 16));
+        put("b256_m16_no_hash_no_lookback", time_variant<256, ABL_NO_HASH | ABL_NO_LOOKBACK>(c, 1, reps, 16));
+        put("b256_m16_no_xcd_local", time_variant<256, ABL_NO_XCD_LOCAL>(c, 1, reps, 16));
+        put("b256_m16_no_hash_no_prologue", time_variant<256, ABL_NO_HASH | ABL_NO_PROLOGUE>(c, 1, reps, 16));
+        put("b256_m16_persist", time_variant<256, ABL_PERSIST>(c, 1, reps, 16));
+        put("b256_m16_persist_no_lookback", time_variant<256, ABL_PERSIST | ABL_NO_LOOKBACK>(c, 1, reps, 16));
+        put("b256_m16_persist_no_lookback_no_hash", time_variant<256, ABL_PERSIST | ABL_NO_LOOKBACK | ABL_NO_HASH>(c, 1, reps, 16));
+        put("b256_m16_persist_load_only", time_variant<256, ABL_PERSIST | ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps, 16));
+        put("b256_m16_persist_no_lines", time_variant<256, ABL_PERSIST | ABL_NO_LINES>(c, 1, reps, 16));
+        put("b256_m16_persist_no_hash", time_variant<256, ABL_PERSIST | ABL_NO_HASH>(c, 1, reps, 16));
         put("b512_m16", time_variant<512, ABL_NONE>(c, 1, reps, 16));
         put("b256_m16_no_hash", time_variant<256, ABL_NO_HASH>(c, 1, reps, 16));
         put("b512_m16_no_hash", time_variant<512, ABL_NO_HASH>(c, 1, reps, 16));
-        put("b256_m16_mfma_hash", time_variant<256, ABL_MFMA_HASH>(c, 1, reps, 16));
-        put("b1024_m16", time_variant<1024, ABL_NONE>(c, 1, reps, 16));
         put("b256_m16", time_variant<256, ABL_NONE>(c, 1, reps, 16));
         put("b512_m16_no_lookback", time_variant<512, ABL_NO_LOOKBACK>(c, 1, reps, 16));
         put("b512_m16_no_lines", time_variant<512, ABL_NO_LINES>(c, 1, reps, 16));
-        put("b512_m16_no_prologue", time_variant<512, ABL_NO_PROLOGUE>(c, 1, reps, 16));
         put("b512_m16_load_only", time_variant<512, ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps, 16));
-        put("b512_m1", time_variant<512, ABL_NONE>(c, 1, reps, 1));
         put("b256_m16_no_lookback", time_variant<256, ABL_NO_LOOKBACK>(c, 1, reps, 16));
         put("b256_m16_no_lines", time_variant<256, ABL_NO_LINES>(c, 1, reps, 16));
         put("b256_m16_load_only", time_variant<256, ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps, 16));
@@ -189,6 +203,20 @@ int main(int argc, char **argv) {
         int bad = 0;
         for (int k = 0; k < 16; ++k) bad += n[k] != lines[k];
         fprintf(stderr, "b512 m16: %d of 16 batch counts wrong\n", bad);
+        CK(hipMemsetAsync(c.d_n, 0xFF, 16 * 8, c.s[0]));
+        launch_route<256, ABL_PERSIST>(c.ds[0], p, c.s[0]);
+        CK(hipMemcpyAsync(n.data(), c.d_n, 16 * 8, hipMemcpyDeviceToHost, c.s[0]));
+        CK(hipStreamSynchronize(c.s[0]));
+        bad = 0;
+        for (int k = 0; k < 16; ++k) bad += n[k] != lines[k];
+        fprintf(stderr, "b256 persist m16: %d of 16 batch counts wrong\n", bad);
+        CK(hipMemsetAsync(c.d_n, 0xFF, 16 * 8, c.s[0]));
+        launch_route<256, ABL_PAIR>(c.ds[0], p, c.s[0]);
+        CK(hipMemcpyAsync(n.data(), c.d_n, 16 * 8, hipMemcpyDeviceToHost, c.s[0]));
+        CK(hipStreamSynchronize(c.s[0]));
+        bad = 0;
+        for (int k = 0; k < 16; ++k) bad += n[k] != lines[k];
+        fprintf(stderr, "b256 pair m16: %d of 16 batch counts wrong\n", bad);
     }
     printf("{\"line_len\": %u, \"batch_bytes\": %zu, \"us_per_batch\": {", line_len, batch);
     for (size_t r = 0; r < rows.size(); ++r) {

@@ -97,9 +97,46 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
     };
     for (int w = 0; w < 3; ++w) launch();
     CK(hipStreamSynchronize(s));
+    CK(hipMemset(d_dbg, 0, h.size() * 8));
     launch();
     CK(hipStreamSynchronize(s));
     CK(hipMemcpy(h.data(), d_dbg, h.size() * 8, hipMemcpyDeviceToHost));
+    {   // record-base chain: tile order per batch (16 batches -> XCD classes j % 8, j and j + 8 share one)
+        std::vector<uint32_t> nt(L);
+        for (int i = 0; i < L; ++i) nt[i] = (uint32_t)((sizes[i] + T - 1) / T);
+        std::vector<std::vector<uint32_t>> order(L);   // per batch: block g of each tile
+        for (uint32_t g = 0; g < total; ++g) {
+            const uint32_t cls = g & 7, ci = g >> 3;
+            const int j = ci < nt[cls] ? (int)cls : (int)cls + 8;
+            const uint32_t t = ci < nt[cls] ? ci : ci - nt[cls];
+            if (j < L && t < nt[j]) {
+                if (order[j].size() <= t) order[j].resize(t + 1, ~0u);
+                order[j][t] = g;
+            }
+        }
+        std::vector<double> late, lag;
+        size_t waited = 0, n = 0;
+        for (int j = 0; j < L; ++j) {
+            uint64_t m = 0;
+            for (size_t t = 0; t < order[j].size(); ++t) {
+                const uint64_t *d = h.data() + (size_t)order[j][t] * 8;
+                ++n;
+                if (d[3]) {
+                    ++waited;
+                    late.push_back(((double)m - (double)d[3]) * 0.01);
+                    lag.push_back(((double)d[7] - (double)std::max(m, d[3])) * 0.01);
+                }
+                m = std::max(m, d[1]);
+            }
+        }
+        std::sort(late.begin(), late.end());
+        std::sort(lag.begin(), lag.end());
+        auto pc = [](std::vector<double> &v, double q) { return v.empty() ? 0.0 : v[(size_t)(q * (v.size() - 1))]; };
+        printf("{\"base_chain\": {\"tiles\": %zu, \"polled\": %zu, \"pred_count_late_us\": [%.2f, %.2f, %.2f, %.2f], "
+               "\"lag_after_counts_us\": [%.2f, %.2f, %.2f, %.2f]}}\n",
+               n, waited, pc(late, 0.1), pc(late, 0.5), pc(late, 0.9), pc(late, 0.99), pc(lag, 0.1), pc(lag, 0.5),
+               pc(lag, 0.9), pc(lag, 0.99));
+    }
     std::vector<double> ph[6];
     uint64_t s0 = ~0ull, e1 = 0;
     for (uint32_t b = 0; b < total; ++b) {
@@ -109,13 +146,14 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
         const double u = 0.01;
         ph[0].push_back((d[1] - d[0]) * u);
         ph[1].push_back((d[2] - d[1]) * u);
-        ph[2].push_back((d[7] - d[3]) * u);   // base wait (tid 0, first record)
+        if (d[3]) ph[2].push_back((d[7] - d[3]) * u);   // base wait (tid 0, first record), when polled
         ph[3].push_back((d[4] - d[2]) * u);
         ph[4].push_back((d[5] - d[4]) * u);
         ph[5].push_back((d[6] - d[0]) * u);
     }
     {
         std::vector<double> w = ph[2];
+        if (w.empty()) w.push_back(0.0);
         std::sort(w.begin(), w.end());
         printf("{\"base_wait_us_percentiles\": {\"p10\": %.2f, \"p50\": %.2f, \"p90\": %.2f, \"p99\": %.2f}}\n",
                w[w.size() / 10], w[w.size() / 2], w[w.size() * 9 / 10], w[w.size() * 99 / 100]);
@@ -154,10 +192,6 @@ int main(int argc, char **argv) {
     CK(hipMalloc(&d_dbg, (size_t)L * 4096 * 8 * 8));
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    run<1024>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
-    run<512>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
-    run<256>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
-    run_many<512>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
     run_many<256>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
     return 0;
 }
