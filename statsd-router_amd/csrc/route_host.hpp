@@ -54,7 +54,6 @@ struct DeviceState {
     uint64_t *d_alive = nullptr;
     Magic *d_magic = nullptr;
     uint64_t *d_kpow = nullptr;
-    uint4 *d_afrag = nullptr;
     Control *d_ctl = nullptr;
     uint64_t *d_status = nullptr;
     uint64_t *d_bases = nullptr;
@@ -70,12 +69,13 @@ struct DeviceState {
         if (!h_alive) return -ENOMEM;
         if (hipMalloc(&d_alive, (nwords ? nwords : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&d_magic, (n_downstreams + 1) * sizeof(Magic)) != hipSuccess) return -ENOMEM;
-        if (hipMalloc(&d_kpow, kPowTable * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+        if (hipMalloc(&d_kpow, (kPowLo + kPowHi + kPowInv) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&d_ctl, sizeof(Control)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&d_status, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&d_bases, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
         if (hipMemset(d_bases, 0, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -EIO;
         if (hipMemset(d_ctl, 0, sizeof(Control)) != hipSuccess) return -EIO;
+
         if (hipMemset(d_status, 0, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -EIO;
         std::vector<Magic> mg(n_downstreams + 1);
         for (uint32_t d = 1; d <= n_downstreams; ++d) {
@@ -88,35 +88,12 @@ struct DeviceState {
         magic_n = n_downstreams ? mg[n_downstreams] : Magic{0, 0, 0};
         if (hipMemcpy(d_magic, mg.data(), mg.size() * sizeof(Magic), hipMemcpyHostToDevice) != hipSuccess)
             return -EIO;
-        std::vector<uint64_t> kp(kPowTable);
-        for (int i = 0; i < 64; ++i) {
-            kp[i] = ipow(K, (unsigned)i);
-            kp[64 + i] = ipow(K, 64u * (unsigned)i);
-            kp[128 + i] = ipow(kKinv, (unsigned)i);
-        }
+        std::vector<uint64_t> kp(kPowLo + kPowHi + kPowInv);
+        for (int i = 0; i < kPowLo; ++i) kp[i] = ipow(K, (unsigned)i);
+        for (int i = 0; i < kPowHi; ++i) kp[kPowLo + i] = ipow(K, 64u * (unsigned)i);
+        for (int z = 0; z < kPowInv; ++z) kp[kPowLo + kPowHi + z] = ipow(kKinv, (unsigned)z);
         if (hipMemcpy(d_kpow, kp.data(), kp.size() * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess)
             return -EIO;
-        // int8 MFMA A fragments (route_kernel.hpp, hash_group): lane l, row r = l & 15, quarter
-        // q = l >> 4, byte j -> signed base-256 digit (r & 3) [+4 for the second table] of K^-(16q+j)
-        {
-            int8_t dig[64][8];
-            for (int pp = 0; pp < 64; ++pp) {
-                uint64_t w = ipow(kKinv, (unsigned)pp);
-                for (int r = 0; r < 8; ++r) {
-                    int d = (int)(w & 0xFF);
-                    if (d >= 128) d -= 256;
-                    dig[pp][r] = (int8_t)d;
-                    w = (w - (uint64_t)(int64_t)d) >> 8;
-                }
-            }
-            std::vector<int8_t> af(2 * 64 * 16);
-            for (int t = 0; t < 2; ++t)
-                for (int l = 0; l < 64; ++l)
-                    for (int j = 0; j < 16; ++j)
-                        af[(t * 64 + l) * 16 + j] = dig[16 * (l >> 4) + j][4 * t + ((l & 15) & 3)];
-            if (hipMalloc(&d_afrag, af.size()) != hipSuccess) return -ENOMEM;
-            if (hipMemcpy(d_afrag, af.data(), af.size(), hipMemcpyHostToDevice) != hipSuccess) return -EIO;
-        }
         for (uint32_t i = 0; i < n_downstreams; ++i) h_alive[i >> 6] |= 1ull << (i & 63);
         if (hipMemcpy(d_alive, h_alive, (nwords ? nwords : 1) * sizeof(uint64_t), hipMemcpyHostToDevice) !=
             hipSuccess)
@@ -129,7 +106,6 @@ struct DeviceState {
         (void)hipFree(d_alive);
         (void)hipFree(d_magic);
         (void)hipFree(d_kpow);
-        (void)hipFree(d_afrag);
         (void)hipFree(d_ctl);
         (void)hipFree(d_status);
         (void)hipFree(d_bases);
@@ -138,7 +114,6 @@ struct DeviceState {
         d_alive = nullptr;
         d_magic = nullptr;
         d_kpow = nullptr;
-        d_afrag = nullptr;
         d_ctl = nullptr;
         d_status = nullptr;
         d_bases = nullptr;
@@ -181,7 +156,6 @@ struct DeviceState {
         p.alive = d_alive;
         p.magic = d_magic;
         p.kpow = d_kpow;
-        p.afrag = d_afrag;
         p.ctl = d_ctl;
         p.status = d_status;
         p.bases = d_bases;
@@ -262,30 +236,7 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
         for (int c = 0; c < 8; ++c) mx = cls_tiles[c] > mx ? cls_tiles[c] : mx;
         grid_tiles = 8 * mx;
     }
-    for (int c = 0; c < 8; ++c) p.cls_tiles[c] = cls_tiles[c];
-    if (ABL & ABL_PAIR) {   // one workgroup per two tiles of a class
-        uint32_t mx = 0;
-        for (int c = 0; c < (xl ? 8 : 1); ++c) mx = (cls_tiles[c] + 1) / 2 > mx ? (cls_tiles[c] + 1) / 2 : mx;
-        grid_tiles = xl ? 8 * mx : mx;
-    }
     p.total_blocks = p.nb + grid_tiles;   // scanners first, then the tiles
-    if (ABL & ABL_PERSIST) {
-        // as many tile workgroups as stay resident beside the scanners, dealt evenly to the classes
-        static int slots = 0;
-        if (!slots) {
-            int occ = 0, dev = 0, cus = 0;
-            if (hipGetDevice(&dev) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, route_kernel<BLOCK, ABL>, BLOCK, 0) != hipSuccess)
-                return -EIO;
-            slots = occ * cus;
-        }
-        uint32_t nwg = (uint32_t)slots > p.nb + 8 ? (uint32_t)slots - p.nb : 8u;
-        if (xl) nwg &= ~7u;
-        if (nwg > grid_tiles) nwg = grid_tiles;
-        p.nwg = nwg;
-        p.total_blocks = p.nb + nwg;
-    }
     if (ds.wide() && hipMemsetAsync(&ds.d_ctl->pending, 0, sizeof(uint32_t), stream) != hipSuccess) return -EIO;
     hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     if (hipGetLastError() != hipSuccess) return -EIO;

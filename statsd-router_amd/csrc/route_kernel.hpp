@@ -52,11 +52,11 @@ constexpr int kTile = kBlock * kLaneBytes;   // 16 KiB per tile
 constexpr int kOverlay = 16;                 // register overlay entries of the probe
 constexpr int kNone = 0x1FFFF;               // "no colon" marker (above any tile position)
 constexpr int kSpinBudget = 1 << 14;         // polls before a missing predecessor is proxied
-constexpr int kLookRounds = 1;               // look-back reach: 64 tiles per round
 constexpr uint32_t kFlagAgg = 1u, kFlagIncl = 2u;
 constexpr uint16_t kRoutePending = 0xFFFCu;  // internal: resolved by probe_wide_kernel
 constexpr uint64_t K = 65599ull;             // sdbm multiplier: (h<<6)+(h<<16)-h (sr-main.c:131)
-constexpr int kPowTable = 192;               // K^i, K^(64 i), K^-i for i < 64 (copied to LDS per tile)
+constexpr int kPowLo = 64, kPowHi = 24;     // K^i (i < 64) and K^(64 i) (i < 24: exponents below 1536)
+constexpr int kPowInv = 4;                   // K^-z (z < 4)
 
 // ablation switches (tools/ablate_route.hip); the product instantiates ABL_NONE
 enum : unsigned {
@@ -69,14 +69,12 @@ enum : unsigned {
     ABL_STAMPS = 32u,       // diagnostic: s_memrealtime at phase boundaries into RouteParams::dbg
     ABL_NO_XCD_LOCAL = 64u, // deal every launch's tiles round-robin even when it has 8+ batches
     ABL_NO_HASH = 256u,     // ablation: skip the sdbm (h = 0); staging, probe and records stay
-    ABL_MFMA_HASH = 128u,   // experiment: name hash as int8 MFMA digit sums (bit-exact, slower: DESIGN.md §6)
-    ABL_PERSIST = 512u,     // persistent tile workgroups: each loops over tiles, loading tile i+1 while routing tile i
+    ABL_LDS_PAD = 131072u,  // occupancy experiment: 4 KiB of unused LDS per workgroup
     ABL_OLD_MASKS = 65536u,  // round-1 v0.5 piece masks (one SWAR test per pattern)
     ABL_OLD_SCANNER = 32768u, // round-1 v0.5 scanner: one wave polls and publishes
-    ABL_DEFER = 16384u,     // the last window's records kept in LDS; base by look-back, then written
-    ABL_PAIR = 8192u,       // two tiles per workgroup: the second's loads and count up front, the first's records late
     ABL_FAKE_BASE = 4096u,  // ablation: base = t * (this tile's count), exact only for uniform tiles (C2)
     ABL_LATE_BASE = 2048u,  // read the record base only after hashing (round-1 v0.5)
+    ABL_AGENT_GRANULES = 262144u,  // every count / base granule stored sc1 (round-1 v0.5), whatever the XCDs
     ABL_OLD_HASH = 1024u,   // round-1 v0.5 per-segment sdbm (v_alignbyte reads, compiler-extracted bytes)
 };
 
@@ -121,7 +119,7 @@ struct Control {
     uint32_t pending;
     uint32_t pad0[29];
     uint32_t done[8][32];
-    uint32_t grab[8][32];   // ABL_PERSIST: next tile of each XCD class (handed out in order)
+    uint64_t scan_xcc[32];   // per batch: the XCD its scanner runs on (kFlagXcc granule)
 };
 
 // One batch of a launch. A launch routes up to kMaxBatches independent batches: tiles
@@ -151,15 +149,12 @@ struct RouteParams {
     Magic magic_n;           // for h % nds (fast path)
     const uint64_t *alive;   // bitmap
     const Magic *magic;      // [0..nds], index i -> divisor i
-    const uint64_t *kpow;    // kPowTable entries: K^i, K^(64 i), K^-i (i < 64)
-    const uint4 *afrag;      // [2][64]: per lane, the int8 MFMA A fragment of limbs 0-3 / 4-7 (hash_group)
+    const uint64_t *kpow;    // kPowLo + kPowHi + kPowInv entries: K^i (i < 64), K^(64 i) (i < 24), K^-z (z < 4)
     Control *ctl;
     uint64_t *status;        // per-tile '\n' count granules {epoch, flag, count} (written by the tile)
     uint64_t *bases;         // per-tile first-record granules {epoch, flag, base} (written by the scanner)
     PendingLine *pending;
     uint64_t *dbg;           // ABL_STAMPS builds only: 8 timestamps per tile
-    uint32_t nwg;            // ABL_PERSIST: tile workgroups of the launch (a multiple of 8 when xcd_local)
-    uint32_t cls_tiles[8];   // tiles per XCD class (class 0 only without xcd_local)
     BatchDesc b[kMaxBatches];
 };
 
@@ -510,32 +505,26 @@ struct SmemT {
     static constexpr int kRows = (kHalo + kTileB) / 64;
     static constexpr int kWords = kRows * 17 + 20;
     uint32_t img[kWords];
-    union {
-        // load -> mask phase: per 16-byte piece P of the tile, its '\n' mask (low 16 bits) and
-        // ':' mask (high 16 bits), computed from the load registers
-        uint32_t pm[BLOCK * 4];
-        struct {
-            int32_t lend[kWin + 1];  // per staged line: tile position of its '\n'; slot 0 = previous
-            int32_t lcol[kWin + 1];  // per staged line: first ':' in the tile part (kNone if none)
-            sr_record rec[kWin];     // the last window's records, written once the base is known
-        };
-    };
-    uint64_t wave_seg[kWaves];
-    uint64_t wave_pre[kWaves];       // exclusive line state of each wave
+    int32_t lend[kWin + 1];          // per staged line: tile position of its '\n'; slot 0 = previous
+    int32_t lcol[kWin + 1];          // per staged line: first ':' in the tile part (kNone if none)
     uint32_t wave_cnt[kWaves];
-    uint32_t wave_cnt2[kWaves];      // pair mode: the second tile's per-wave '\n' counts
     uint32_t wave_scan[kWaves][4];   // per wave, inclusive at its last lane: '\n' count, latest '\n' lane, colon key
-    uint64_t kp_lo[64];              // K^i
-    uint64_t kp_hi[64];              // K^(64 i)
-    uint64_t kinv[64];               // K^-i
-    uint32_t kmask[17][4];           // kmask[n]: 16-byte mask keeping the first n bytes
+    uint64_t kp_lo[kPowLo];          // K^i
+    uint64_t kp_hi[kPowHi];          // K^(64 i)
+    uint64_t kp_inv[kPowInv];        // K^-z (an LDS read rather than three 64-bit constants held in VGPRs)
+    static constexpr int kPowWords = (kPowLo + kPowHi + kPowInv) * 2;   // u32 words of the three tables
     int32_t s_pre, c_pre;            // straddling line: tile-relative start / first colon before T0
     uint32_t epoch, base;
-    uint32_t grab, grab0;            // ABL_PERSIST: tile indices handed to this workgroup
     uint32_t scan_head, scan_pub, scan_total;   // scanner: bases computed / published, line total
 };
 
-// K^n for 0 <= n < 4096 from the LDS tables
+// K^-z for z = 1, 2, 3 (undoing z bytes of zero padding)
+__device__ __forceinline__ uint64_t kinv_small(int z) {
+    constexpr uint64_t i1 = kKinv, i2 = kKinv * kKinv, i3 = kKinv * kKinv * kKinv;
+    return z == 1 ? i1 : (z == 2 ? i2 : i3);
+}
+
+// K^n for 0 <= n < 1536 from the LDS tables
 template <class S>
 __device__ __forceinline__ uint64_t kpow_n(const S &sm, int n) {
     return sm.kp_hi[n >> 6] * sm.kp_lo[n & 63];
@@ -566,7 +555,7 @@ __device__ __forceinline__ uint64_t sdbm_lds(const S &sm, int a, int n) {
         for (int m = 0; m < 16; ++m)
             if (m == nfull) x = __builtin_amdgcn_alignbyte(w[m + 1], w[m], sh);
         x &= (1u << (8 * rem)) - 1u;
-        h = sdbm_dword(h, x) * sm.kinv[4 - rem];
+        h = sdbm_dword(h, x) * kinv_small(4 - rem);
     }
     return h;
 }
@@ -582,12 +571,12 @@ __device__ __forceinline__ uint64_t sdbm_img(const S &sm, int a, int n) {
     const int dw = a >> 2, s16 = dw & 15, cross = 16 - s16;
     const uint32_t *const p = &sm.img[(dw >> 4) * 17 + s16];
     const uint32_t first = p[0] & (0xFFFFFFFFu << (8 * lead));
-    if (F == 0) return sdbm_dword_fast(0, first & ((1u << (8 * rem)) - 1u)) * sm.kinv[4 - rem];
+    if (F == 0) return sdbm_dword_fast(0, first & ((1u << (8 * rem)) - 1u)) * sm.kp_inv[4 - rem];
     uint64_t h = sdbm_dword_fast(0, first);
     int m = 1;
     for (; m < F && m < cross; ++m) h = sdbm_dword_fast(h, p[m]);
     for (; m < F; ++m) h = sdbm_dword_fast(h, p[m + 1]);
-    if (rem) h = sdbm_dword_fast(h, p[m + (m >= cross ? 1 : 0)] & ((1u << (8 * rem)) - 1u)) * sm.kinv[4 - rem];
+    if (rem) h = sdbm_dword_fast(h, p[m + (m >= cross ? 1 : 0)] & ((1u << (8 * rem)) - 1u)) * sm.kp_inv[4 - rem];
     return h;
 }
 
@@ -629,6 +618,26 @@ __device__ uint32_t count_tile_wave(uint32_t nbytes, __amdgpu_buffer_rsrc_t rsrc
 // A tile whose count has not appeared within the spin budget is counted by the scanner itself,
 // so the scan completes whatever the dispatch order.
 constexpr uint32_t kFlagBase = 2u;
+constexpr uint32_t kFlagXcc = 3u;
+// A tile's count granule carries (8 | its XCD) in bits 28..31 of the value above the count.
+constexpr uint32_t kCountMask = 0x0FFFFFFFu;
+
+// XCD of the executing workgroup. Placement is observed, never assumed: a granule whose producer
+// and consumer share an XCD is stored plain (the line stays in that XCD's L2, where the consumer's
+// sc1 poll finds it); any other granule is stored sc1 (written through, dropped from L2).
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+    return x;
+}
+
+// 8-byte granule store: plain when the reader shares this XCD, else sc1 (agent scope)
+__device__ __forceinline__ void granule_store(uint64_t *slot, uint64_t v, bool same_xcd) {
+    if (same_xcd)
+        __hip_atomic_store(slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else
+        __hip_atomic_store(slot, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 __device__ __forceinline__ bool granule_ok(uint64_t st, uint32_t ep, uint32_t flag) {
     return (uint32_t)(st >> 34) == ep && ((st >> 32) & 3u) == flag;
@@ -657,7 +666,7 @@ __device__ void scan_batch(const RouteParams &p, const BatchDesc &bd, uint32_t e
             if (!have[k]) {
                 const uint64_t st = __hip_atomic_load(&status[tt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (granule_ok(st, ep, kFlagAgg)) {
-                    cnt[k] = (uint32_t)st;
+                    cnt[k] = (uint32_t)st & kCountMask;
                     have[k] = true;
                 }
             }
@@ -708,7 +717,7 @@ __device__ void scan_batch(const RouteParams &p, const BatchDesc &bd, uint32_t e
 // poll. Wave 0 polls the tiles' counts and computes their bases into an LDS ring (head index
 // released after the writes); wave 1 publishes the ring to the bases granules and the batch's
 // line count. Flow control keeps the ring (the LDS image, 4096 entries) from overrunning.
-template <int BLOCK>
+template <int BLOCK, bool kAgentOnly>
 __device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint32_t epoch, SmemT<BLOCK> &sm,
                                  int wave, int lane) {
     constexpr uint32_t kRing = 4096;
@@ -720,6 +729,11 @@ __device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint
         const __amdgpu_buffer_rsrc_t rsrc =
             __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
         const uint32_t ep = epoch & 0x3FFFFFFFu;
+        // tiles that share this XCD get their base by a plain store (ring entry bit 31)
+        const uint32_t mine = kAgentOnly ? 0u : (8u | xcc_id()) << 28;
+        if (lane == 0 && !kAgentOnly)
+            __hip_atomic_store(&p.ctl->scan_xcc[blockIdx.x], mk_status(epoch, kFlagXcc, xcc_id()), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         uint32_t run = 0, c = 0;
         int spin = 0;
         while (c < bd.ntiles) {
@@ -727,17 +741,19 @@ __device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint
             while (c + 64 * kGroups > __hip_atomic_load(&sm.scan_pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) +
                                           kRing)
                 __builtin_amdgcn_s_sleep(1);
-            uint32_t cnt[kGroups];
+            uint32_t cnt[kGroups], loc[kGroups];
             bool have[kGroups];
 #pragma unroll
             for (int k = 0; k < kGroups; ++k) {
                 const uint32_t tt = c + 64 * k + lane;
                 cnt[k] = 0;
+                loc[k] = 0;
                 have[k] = tt >= bd.ntiles;
                 if (!have[k]) {
                     const uint64_t st = __hip_atomic_load(&status[tt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (granule_ok(st, ep, kFlagAgg)) {
-                        cnt[k] = (uint32_t)st;
+                        cnt[k] = (uint32_t)st & kCountMask;
+                        loc[k] = ((uint32_t)st & ~kCountMask) == mine && mine ? 0x80000000u : 0u;
                         have[k] = true;
                     }
                 }
@@ -762,7 +778,7 @@ __device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint
                 if (nready == 0) break;
                 const uint32_t v = lane < nready ? cnt[k] : 0u;
                 const uint32_t incl = wave_incl_add32(v);
-                if (lane < nready && c + lane < bd.ntiles) ring[(c + lane) % kRing] = run + incl - v;
+                if (lane < nready && c + lane < bd.ntiles) ring[(c + lane) % kRing] = (run + incl - v) | loc[k];
                 run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                 c += (uint32_t)nready;
                 if (nready < 64 || c >= bd.ntiles) break;
@@ -788,9 +804,10 @@ __device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint
                 __builtin_amdgcn_s_sleep(1);
                 continue;
             }
-            for (uint32_t i = pub + lane; i < h; i += 64)
-                __hip_atomic_store(&bases[i], mk_status(epoch, kFlagBase, ring[i % kRing]), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            for (uint32_t i = pub + lane; i < h; i += 64) {
+                const uint32_t r = ring[i % kRing];
+                granule_store(&bases[i], mk_status(epoch, kFlagBase, r & 0x7FFFFFFFu), (r >> 31) != 0u);
+            }
             pub = h;
             if (lane == 0) __hip_atomic_store(&sm.scan_pub, pub, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
@@ -814,76 +831,6 @@ __device__ uint32_t wait_base(const uint64_t *slot, uint32_t epoch, __amdgpu_buf
     return n;
 }
 
-// ---- name hash on the matrix cores -----------------------------------------------------------
-// For a 64-byte segment of a name starting at byte a (name bytes c_0 .. c_{n-1}), with
-// W_p = K^-p mod 2^64 written in signed base-256 digits W_p = sum_r d_r(p) 256^r (d in [-128, 127]):
-//     T = sum_p c_p W_p = sum_r 256^r C_r,   C_r = sum_p c_p d_r(p)   (exact int32, |C_r| < 2^21)
-// and the sdbm of the whole name is  h = sum_k K^(n-1-64k) T_k  (mod 2^64) over its segments k.
-// One v_mfma_i32_16x16x64_i8 computes C_r for 16 segments (B columns = segments, 16 bytes per
-// lane, A rows = digits). A wave hashes 64 lines at a time: MFMA m takes the lines 16m .. 16m+15
-// with its digits in A rows 4m .. 4m+3, so its results land in rows 4m .. 4m+3 = lanes 16m .. 16m+15
-// (column = lane & 15): after the four MFMAs of a limb half, lane l holds the digit sums of line l.
-typedef int v4i_t __attribute__((ext_vector_type(4)));
-
-template <class S>
-__device__ __forceinline__ v4i_t gather16(const S &sm, int a, int keep) {
-    // image bytes [a, a + 16), only the first `keep` (0..16) kept, as the MFMA's 16 int8
-    v4i_t out = {0, 0, 0, 0};
-    if (keep > 0) {
-        const int base = a & ~3, sh = a & 3;
-        const int i0 = img_dw(base), r0 = base & 63;
-        uint32_t w[5];
-#pragma unroll
-        for (int m = 0; m < 5; ++m) w[m] = sm.img[i0 + m + ((r0 + 4 * m) >> 6)];
-        const uint32_t *mk = sm.kmask[keep];
-#pragma unroll
-        for (int d = 0; d < 4; ++d) out[d] = (int)(__builtin_amdgcn_alignbyte(w[d + 1], w[d], sh) & mk[d]);
-    }
-    return out;
-}
-
-// Hash of the 64 lines of a wave: lane l's line starts at image byte a_l and has n_l name bytes
-// (0: no hash). Returns lane l's h.
-template <class S>
-__device__ __forceinline__ uint64_t hash_group(const S &sm, const uint4 *afrag, int a_me, int n_me, int lane) {
-    const int q = lane >> 4, col = lane & 15, rowgrp = col >> 2;
-    int kmax = (n_me + 63) >> 6;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) kmax = max(kmax, __shfl_xor(kmax, d, 64));
-    const v4i_t z = {0, 0, 0, 0};
-    const uint4 f1 = afrag[lane], f2 = afrag[64 + lane];
-    uint64_t h = 0;
-    for (int k = 0; k < kmax; ++k) {
-        v4i_t lo = z, hi = z;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            // the line of MFMA m this lane feeds (16m + col), its bytes [64k + 16q, +16)
-            const int am = __shfl(a_me, 16 * m + col, 64), nm = __shfl(n_me, 16 * m + col, 64);
-            const int off = 64 * k + 16 * q;
-            const int keep = min(max(nm - off, 0), 16);
-            const v4i_t b = gather16(sm, am + off, keep);
-            // this lane's A rows carry digits only in MFMA m == its row group (the select is
-            // re-done per MFMA: an opaque copy keeps the compiler from holding 8 fragments)
-            uint4 g1 = f1, g2 = f2;
-            asm volatile("" : "+v"(g1.x), "+v"(g1.y), "+v"(g1.z), "+v"(g1.w));
-            asm volatile("" : "+v"(g2.x), "+v"(g2.y), "+v"(g2.z), "+v"(g2.w));
-            const bool on = rowgrp == m;
-            const v4i_t F1 = {on ? (int)g1.x : 0, on ? (int)g1.y : 0, on ? (int)g1.z : 0, on ? (int)g1.w : 0};
-            const v4i_t F2 = {on ? (int)g2.x : 0, on ? (int)g2.y : 0, on ? (int)g2.z : 0, on ? (int)g2.w : 0};
-            lo = __builtin_amdgcn_mfma_i32_16x16x64_i8(F1, b, lo, 0, 0, 0);
-            hi = __builtin_amdgcn_mfma_i32_16x16x64_i8(F2, b, hi, 0, 0, 0);
-        }
-        if (n_me > 64 * k) {
-            const int32_t p01 = lo[0] + (lo[1] << 8), p23 = lo[2] + (lo[3] << 8);
-            const int32_t p45 = hi[0] + (hi[1] << 8), p67 = hi[2] + (hi[3] << 8);
-            const uint64_t T = (uint64_t)(int64_t)p01 + ((uint64_t)(int64_t)p23 << 16) +
-                               ((uint64_t)((uint32_t)p45 + ((uint32_t)p67 << 16)) << 32);
-            h += T * kpow_n(sm, n_me - 1 - 64 * k);
-        }
-    }
-    return h;
-}
-
 // Arrivals: every block adds itself to a sharded counter (no return value, nothing waits); the
 // last block waits until all have arrived, then resets the counters and advances the epoch.
 // Every block read the epoch before arriving, so none of this launch can see the new one.
@@ -901,7 +848,6 @@ __device__ void arrive(const RouteParams &p, uint32_t blk, uint32_t epoch) {
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) {
         __hip_atomic_store(&p.ctl->done[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&p.ctl->grab[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __hip_atomic_store(&p.ctl->epoch, epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -911,8 +857,9 @@ struct KernelTraits {
     // waves per SIMD to reserve registers for: 1024-thread tiles run one workgroup per CU,
     // smaller tiles several (LDS: 86 KB / 45 KB / 24 KB per workgroup); persistent workgroups
     // hold a second tile in registers and hide latency by prefetch instead of occupancy
-    static constexpr int kMinWavesPerSimd = (ABL & ABL_PERSIST) ? 4 : (ABL & ABL_PAIR) ? 5 : (BLOCK >= 1024 ? 4 : 6);
-    static constexpr int kMaxWavesPerSimd = (ABL & ABL_PERSIST) ? 4 : (ABL & ABL_PAIR) ? 5 : 8;
+    static constexpr int kMinWavesPerSimd = BLOCK >= 1024 ? 4 : (BLOCK >= 512 ? 6 : 7);
+    static constexpr int kMaxWavesPerSimd = 8;
+    static constexpr int kMaxVgpr = 512 / kMinWavesPerSimd / 8 * 8;   // 72 for 7 waves per SIMD
 };
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, never for its
@@ -927,10 +874,12 @@ __device__ __forceinline__ uint32_t batch_of(const RouteParams &p, uint32_t cls,
     return bi;
 }
 
-// One tile's input as loaded into registers: piece P = k*BLOCK + tid of the tile (bytes 16P ..) in
-// v[k]; threads below kHalo/16 also hold 16 bytes of the 2 KiB before the tile.
+// One tile's input as loaded into registers: thread tid holds the tile's bytes [64 tid, 64 tid + 64)
+// in v[0..3] (its own chunk: every wave-instruction still reads one contiguous 4 KiB span), and
+// threads below kHalo/16 hold 16 bytes of the 2 KiB before the tile.
 struct TileIn {
     uint32_t bi, t;
+    uint64_t sx;   // the batch scanner's kFlagXcc granule
     uint4 v[4];
     uint4 hv;
 };
@@ -945,20 +894,23 @@ __device__ __forceinline__ void tile_issue(const RouteParams &p, uint32_t bi, ui
         __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
     in.bi = bi;
     in.t = t;
+    in.sx = (ABL & ABL_AGENT_GRANULES) ? 0ull
+                                       : __hip_atomic_load(&p.ctl->scan_xcc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     in.hv = make_uint4(0, 0, 0, 0);
     if (tid < kHalo / 16 && t > 0 && !(ABL & ABL_NO_PROLOGUE))   // zeros before the batch start
         in.hv = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, T0 - kHalo + tid * 16, 0, 0));
 #pragma unroll
-    for (int k = 0; k < 4; ++k) in.v[k] = load16(rsrc, T0 + k * BLOCK * 16 + tid * 16, bd.nbytes);
+    for (int k = 0; k < 4; ++k) in.v[k] = load16(rsrc, T0 + tid * kLaneBytes + k * 16, bd.nbytes);
 }
 
 // Route one tile (reference: sr-main.c:175-189 + process_data_line + hash + find_downstream's
 // choice, for every line that ends in the tile), in two halves. First half: the tile's bytes from
-// the registers of `in` into the LDS image, the '\n' / ':' masks of every piece, and the tile's
-// '\n' count published for the scanner. Needs the LDS free of the previous tile's readers.
+// the registers of `in` into the LDS image (thread tid's chunk = image row tid), the '\n' / ':'
+// masks of the thread's 64 bytes (bit i = byte 64 tid + i) into nlm / clm, and the tile's '\n'
+// count published for the scanner.
 template <int BLOCK, unsigned ABL>
-__device__ __forceinline__ void tile_load_lds(const RouteParams &p, SmemT<BLOCK> &sm, const TileIn &in, uint32_t epoch,
-                                              uint32_t g) {
+__device__ __forceinline__ void tile_load(const RouteParams &p, SmemT<BLOCK> &sm, const TileIn &in, uint32_t epoch,
+                                          uint32_t g, uint64_t &nlm, uint64_t &clm) {
     using S = SmemT<BLOCK>;
     constexpr int kWaves = S::kWaves;
     constexpr int kHalo = S::kHalo;
@@ -969,20 +921,25 @@ __device__ __forceinline__ void tile_load_lds(const RouteParams &p, SmemT<BLOCK>
 
     stamp<ABL>(p, tid, g, 0);
     if (tid < kHalo / 16) img_put16(sm, tid * 16, in.hv);
-    // the '\n' / ':' masks of each piece are taken from the registers (-> sm.pm) and the '\n' count
-    // with them, so the tile's aggregate can be published early
     {
-        uint32_t cnt = 0;
+        uint32_t *const row = &sm.img[(kHalo / 64 + tid) * 17];   // 17-dword rows: conflict-free per-lane rows
+        uint32_t m[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            img_put16(sm, kHalo + 16 * (k * BLOCK + tid), in.v[k]);
-            uint32_t m;
-            if (ABL & ABL_OLD_MASKS) m = eq_mask16_dot(in.v[k], 0x0A0A0A0Au) | (eq_mask16_dot(in.v[k], 0x3A3A3A3Au) << 16);
-            else m = nl_colon_mask16(in.v[k]);
-            sm.pm[k * BLOCK + tid] = m;
-            cnt += __popc(m & 0xFFFFu);
+            row[4 * k] = in.v[k].x;
+            row[4 * k + 1] = in.v[k].y;
+            row[4 * k + 2] = in.v[k].z;
+            row[4 * k + 3] = in.v[k].w;
+            if (ABL & ABL_OLD_MASKS)
+                m[k] = eq_mask16_dot(in.v[k], 0x0A0A0A0Au) | (eq_mask16_dot(in.v[k], 0x3A3A3A3Au) << 16);
+            else
+                m[k] = nl_colon_mask16(in.v[k]);
         }
-        cnt = wave_add32(cnt);
+        nlm = ((uint64_t)__builtin_amdgcn_perm(m[3], m[2], 0x05040100u) << 32) |
+              __builtin_amdgcn_perm(m[1], m[0], 0x05040100u);
+        clm = ((uint64_t)__builtin_amdgcn_perm(m[3], m[2], 0x07060302u) << 32) |
+              __builtin_amdgcn_perm(m[1], m[0], 0x07060302u);
+        const uint32_t cnt = wave_add32((uint32_t)__popcll(nlm));
         if (lane == 0) sm.wave_cnt[wave] = cnt;
     }
     wg_barrier();
@@ -991,17 +948,18 @@ __device__ __forceinline__ void tile_load_lds(const RouteParams &p, SmemT<BLOCK>
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) tile_count += sm.wave_cnt[w];
     if (tid == 0) {   // publish this tile's '\n' count for the scanner
-        const uint64_t st = mk_status(epoch, kFlagAgg, tile_count);
-        __hip_atomic_store(&status[in.t], st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t x = xcc_id();
+        const bool same = !(ABL & ABL_AGENT_GRANULES) && granule_ok(in.sx, epoch & 0x3FFFFFFFu, kFlagXcc) &&
+                          (uint32_t)in.sx == x;
+        granule_store(&status[in.t], mk_status(epoch, kFlagAgg, tile_count | ((8u | x) << 28)), same);
     }
 }
 
-// Second half: lines, hashes, shards and records of the tile whose bytes tile_load_lds left in the
-// LDS. Ends with every LDS reader done (the next tile may overwrite the image).
+// Second half: lines, hashes, shards and records of the tile whose bytes tile_load left in the
+// LDS image and whose chunk masks are in nlm / clm.
 template <int BLOCK, unsigned ABL>
-__device__ __forceinline__ uint2 tile_lines(const RouteParams &p, SmemT<BLOCK> &sm, const TileIn &in, uint32_t epoch,
-                                            uint32_t g, sr_record *defer = nullptr) {
-    uint2 deferred = make_uint2(0u, 0u);   // {first tile-local line, lines} of the records left in `defer`
+__device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &sm, const TileIn &in, uint32_t epoch,
+                                           uint32_t g, uint64_t nlm, uint64_t clm) {
     stamp<ABL>(p, threadIdx.x, g, 1);
     using S = SmemT<BLOCK>;
     constexpr int kWaves = S::kWaves;
@@ -1026,18 +984,7 @@ __device__ __forceinline__ uint2 tile_lines(const RouteParams &p, SmemT<BLOCK> &
         wg_barrier();
     } else {
     // ---- per lane: '\n' / ':' masks of its 64 contiguous bytes, segmented line-state scan -------
-    const int o = tid * kLaneBytes;   // tile position of the lane's first byte
-    uint64_t nlm, clm;                // bit i: byte o+i is '\n' / ':'
-    {
-        // the lane's pieces 4 tid .. 4 tid + 3 (one 16-byte LDS read); v_perm gathers the halves
-        const uint4 q = *(const uint4 *)&sm.pm[4 * tid];
-        const uint32_t n_lo = __builtin_amdgcn_perm(q.y, q.x, 0x05040100u);
-        const uint32_t n_hi = __builtin_amdgcn_perm(q.w, q.z, 0x05040100u);
-        const uint32_t c_lo = __builtin_amdgcn_perm(q.y, q.x, 0x07060302u);
-        const uint32_t c_hi = __builtin_amdgcn_perm(q.w, q.z, 0x07060302u);
-        nlm = ((uint64_t)n_hi << 32) | n_lo;
-        clm = ((uint64_t)c_hi << 32) | c_lo;
-    }
+    const int o = tid * kLaneBytes;   // tile position of the lane's first byte (nlm / clm bit i: byte o + i)
     const int ncnt = __popcll(nlm);
     // Line state before each lane's chunk, by three u32 wave scans (DPP) and a prefix over the
     // earlier waves: the number of '\n' before it, and the first ':' of the line open at its start.
@@ -1183,80 +1130,10 @@ __device__ __forceinline__ uint2 tile_lines(const RouteParams &p, SmemT<BLOCK> &
         uint64_t st_early = 0;
         if (!have_base && !(ABL & ABL_LATE_BASE))
             st_early = __hip_atomic_load(base_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // Deferred records (the tile's last window): the records are kept in LDS and written after
-        // the window loop, once wave 0 has the base. Wave 0 reads ahead the granules of the kLook
-        // tiles before this one (lane i, round r: tile t-1-64r-i), for a look-back that does not wait
-        // for the scanner: base(t) = base(j) + counts of j .. t-1, j the nearest tile whose base is
-        // published (by the scanner or by a tile's own look-back) with every count in between.
-        const bool defer_tile = (ABL & ABL_DEFER) && !have_base && wbase + kWin >= (int)tile_count && !bd.hashes &&
-                                p.dead <= (uint32_t)kOverlay;
-        uint64_t lb_cnt[kLookRounds], lb_base[kLookRounds];
-#pragma unroll
-        for (int r = 0; r < kLookRounds; ++r) {
-            lb_cnt[r] = 0;
-            lb_base[r] = 0;
-            const int jt = (int)t - 1 - 64 * r - lane;
-            if (defer_tile && wave == 0 && jt >= 0) {
-                lb_cnt[r] = __hip_atomic_load(p.status + bd.sbase + jt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                lb_base[r] = __hip_atomic_load(p.bases + bd.sbase + jt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        if ((ABL & ABL_MFMA_HASH) && !(ABL & ABL_NO_LINES)) {
-            // 64 lines per wave at a time; lane l owns line grp*64 + l (hash on the matrix cores)
+        if (!(ABL & ABL_NO_LINES)) {
             const int s_pre = sm.s_pre;
             const int c_pre = sm.c_pre;
             const int nwin = min(kWin, (int)tile_count - wbase);
-            for (int grp = wave; grp * 64 < nwin; grp += kWaves) {
-                const int jj = grp * 64 + lane;
-                const bool mine = jj < nwin;
-                const int j = wbase + jj;
-                int s = 0, e = 0, c = kNone;
-                if (mine) {
-                    e = sm.lend[jj + 1];
-                    c = sm.lcol[jj + 1];
-                    if (j == 0 && c_pre != kNone) c = c_pre;   // the straddling line's ':' lies before T0
-                    s = (j == 0) ? s_pre : sm.lend[jj] + 1;
-                }
-                const int len = e - s + 1;
-                const bool len_ok = len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH;   // :180
-                const bool fmt_ok = c != kNone && c < e;                                                // :140
-                const int n = (mine && len_ok && fmt_ok) ? c - s : 0;
-                const uint64_t h = hash_group(sm, p.afrag, kHalo + s, n, lane);
-                if (mine) {
-                    uint32_t route;
-                    if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
-                    else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
-                    else route = probe_shard(h, p);                                                    // :145
-                    if (!have_base) {   // needed only now, after the hash: normally long published
-                        stamp<ABL>(p, tid, g, 3);
-                        base = granule_ok(st_early, epoch & 0x3FFFFFFFu, kFlagBase)
-                                   ? (uint32_t)st_early
-                                   : wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
-                        stamp<ABL>(p, tid, g, 7);
-                        have_base = true;
-                    }
-                    const uint32_t rec = base + (uint32_t)j;
-                    if (rec < bd.max_records) {
-                        if (route == kRoutePending) {
-                            const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
-                            if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
-                        }
-                        sr_record r;
-                        r.offset = (uint32_t)(T0 + s);
-                        r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
-                        r.route = (uint16_t)route;
-                        bd.recs[rec] = r;
-                        if (bd.hashes) bd.hashes[rec] = h;
-                    }
-                }
-            }
-        } else if (!(ABL & ABL_NO_LINES)) {
-            const int s_pre = sm.s_pre;
-            const int c_pre = sm.c_pre;
-            const int nwin = min(kWin, (int)tile_count - wbase);
-            // the records of the tile's last window may be left in `defer` (no base wait here)
-            const bool defer_win = (defer != nullptr && wbase + kWin >= (int)tile_count) || defer_tile;
-            sr_record *const dbuf = defer != nullptr ? defer : sm.rec;
             // lanes per line from the mean line length: 64-byte hash segments per lane
             const int mean = kTileB / max((int)tile_count, 1);
             int G = 1;
@@ -1295,9 +1172,7 @@ __device__ __forceinline__ uint2 tile_lines(const RouteParams &p, SmemT<BLOCK> &
                     r.offset = (uint32_t)(T0 + s);
                     r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
                     r.route = (uint16_t)route;
-                    if (defer_win) {   // the record base is read later
-                        dbuf[jj] = r;
-                    } else {
+                    {
                         if (!have_base) {   // needed only now, after the hash: normally long published
                             stamp<ABL>(p, tid, g, 3);
                             base = granule_ok(st_early, epoch & 0x3FFFFFFFu, kFlagBase)
@@ -1318,53 +1193,8 @@ __device__ __forceinline__ uint2 tile_lines(const RouteParams &p, SmemT<BLOCK> &
                     }
                 }
             }
-            if (defer_win) deferred = make_uint2((uint32_t)wbase, (uint32_t)nwin);
         }
-        if (defer_tile && deferred.y) {   // the window loop ends here
-            wg_barrier();   // every record of the window is in sm.rec
-            if (wave == 0) {
-                const uint32_t ep = epoch & 0x3FFFFFFFu;
-                uint32_t b = 0;
-                bool ok = granule_ok(st_early, ep, kFlagBase);
-                if (ok) b = (uint32_t)st_early;
-                uint32_t acc = 0;
-#pragma unroll
-                for (int r = 0; r < kLookRounds; ++r) {
-                    if (ok) break;
-                    const int jt = (int)t - 1 - 64 * r - lane;
-                    const bool okc = jt < 0 || granule_ok(lb_cnt[r], ep, kFlagAgg);
-                    const bool okb = jt == -1 || (jt >= 0 && granule_ok(lb_base[r], ep, kFlagBase));
-                    const uint64_t mc = __ballot(okc), mb = __ballot(okb);
-                    const uint64_t have = ~mc ? ((1ull << __builtin_ctzll(~mc)) - 1ull) : ~0ull;
-                    const uint64_t cands = mb & have;
-                    const uint32_t cv = jt >= 0 ? (uint32_t)lb_cnt[r] : 0u;
-                    if (cands) {
-                        const int i = __builtin_ctzll(cands);
-                        const uint32_t bj = jt >= 0 ? (uint32_t)lb_base[r] : 0u;
-                        b = (uint32_t)__builtin_amdgcn_readlane((int)bj, i) + acc + wave_add32(lane <= i ? cv : 0u);
-                        ok = true;
-                    } else if (~mc) {
-                        break;   // a count missing before any anchor
-                    } else {
-                        acc += wave_add32(cv);
-                    }
-                }
-                if (!ok) b = wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
-                if (lane == 0) {
-                    sm.base = b;
-                    // published for the look-backs of later tiles (the scanner writes the same value)
-                    __hip_atomic_store((uint64_t *)base_slot, mk_status(epoch, kFlagBase, b), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            wg_barrier();
-            const uint32_t b0 = sm.base + (uint32_t)wbase;
-            for (uint32_t i = (uint32_t)tid; i < deferred.y; i += BLOCK) {
-                const uint32_t rec = b0 + i;
-                if (rec < bd.max_records) bd.recs[rec] = sm.rec[i];
-            }
-            deferred = make_uint2(0u, 0u);
-        }
+
         wg_barrier();
         if (wbase == 0) stamp<ABL>(p, tid, g, 5);
         if (tid == 0) sm.lend[0] = sm.lend[min(kWin, (int)tile_count - wbase)];
@@ -1372,41 +1202,6 @@ __device__ __forceinline__ uint2 tile_lines(const RouteParams &p, SmemT<BLOCK> &
     }
     }
     stamp<ABL>(p, tid, g, 6);
-    return deferred;
-}
-
-// Write the records tile_lines left in `buf` (after its closing barrier): the tile's record base
-// has been published by now in all but rare cases, so the poll normally succeeds at once.
-template <int BLOCK>
-__device__ __forceinline__ void flush_records(const RouteParams &p, const TileIn &in, const sr_record *buf, uint2 d,
-                                              uint32_t epoch) {
-    if (d.y == 0) return;
-    const BatchDesc &bd = p.b[in.bi];
-    const uint32_t T0 = in.t * (uint32_t)(BLOCK * kLaneBytes);
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
-    const uint32_t base = wait_base(p.bases + bd.sbase + in.t, epoch, rsrc, T0) + d.x;
-    for (uint32_t i = threadIdx.x; i < d.y; i += BLOCK) {
-        const uint32_t rec = base + i;
-        if (rec < bd.max_records) bd.recs[rec] = buf[i];
-    }
-}
-
-// Pair mode: the second tile's bytes stay in registers while the first is routed; its masks and
-// '\n' count are taken from the registers up front (count published early), then this writes its
-// LDS image and piece masks. Needs the LDS free of the first tile's readers.
-template <int BLOCK, unsigned ABL>
-__device__ __forceinline__ void tile_store_lds(SmemT<BLOCK> &sm, const TileIn &in, const uint32_t pm[4]) {
-    constexpr int kHalo = SmemT<BLOCK>::kHalo;
-    const int tid = threadIdx.x;
-    if (tid < kHalo / 16) img_put16(sm, tid * 16, in.hv);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        img_put16(sm, kHalo + 16 * (k * BLOCK + tid), in.v[k]);
-        sm.pm[k * BLOCK + tid] = pm[k];
-    }
-    if (tid < SmemT<BLOCK>::kWaves) sm.wave_cnt[tid] = sm.wave_cnt2[tid];
-    wg_barrier();
 }
 
 template <int BLOCK, unsigned ABL>
@@ -1417,6 +1212,11 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
+    if (ABL & ABL_LDS_PAD) {   // occupancy experiment: 4 KiB more LDS per workgroup
+        __shared__ uint32_t pad[1024];
+        if (p.nb > 1000000u) pad[tid] = tid;   // never true: keeps the array
+        if (p.nb > 1000000u) p.ctl->pad1 = pad[(tid + 1) & 1023];
+    }
     if (blockIdx.x < p.nb) {   // scanner of batch blockIdx.x (wave 0; no barriers on this path)
         const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (ABL & ABL_OLD_SCANNER) {
@@ -1429,7 +1229,7 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
                 sm.scan_total = 0;
             }
             wg_barrier();
-            scan_batch_split<BLOCK>(p, p.b[blockIdx.x], ep0, sm, wave, lane);
+            scan_batch_split<BLOCK, (ABL & ABL_AGENT_GRANULES) != 0>(p, p.b[blockIdx.x], ep0, sm, wave, lane);
             if (tid == 64) arrive(p, blockIdx.x, ep0);   // the publisher, after its last store
         }
         return;
@@ -1441,110 +1241,18 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     const uint32_t cls = p.xcd_local ? (g & 7u) : 0u;
     uint32_t ci = p.xcd_local ? (g >> 3) : g;
     const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (ABL & ABL_PAIR) {   // tiles 2ci and 2ci + 1 of the class
-        __shared__ sr_record rec_buf[S::kWin];
-        const uint32_t c0 = 2 * ci, c1 = c0 + 1;
-        const uint32_t b0 = batch_of(p, cls, c0);
-        if (b0 == kMaxBatches) {
-            if (tid == 0) arrive(p, blockIdx.x, ep0);
-            return;
-        }
-        const uint32_t b1 = batch_of(p, cls, c1);
-        const bool has_b = b1 != kMaxBatches;
-        TileIn ta, tb;
-        tile_issue<BLOCK, ABL>(p, b0, c0 - p.b[b0].tile0, ta, tid);
-        if (has_b) tile_issue<BLOCK, ABL>(p, b1, c1 - p.b[b1].tile0, tb, tid);
-        if (tid < kPowTable) (&sm.kp_lo[0])[tid] = p.kpow[tid];
-        if (tid < 68) {
-            const int n = tid >> 2, d = tid & 3, kb = min(max(n - 4 * d, 0), 4);
-            sm.kmask[n][d] = kb == 4 ? 0xFFFFFFFFu : ((1u << (8 * kb)) - 1u);
-        }
-        if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
-        tile_load_lds<BLOCK, ABL>(p, sm, ta, ep0, g);
-        uint32_t pmb[4] = {0u, 0u, 0u, 0u};
-        if (has_b) {   // the second tile's masks and count from its registers; count published now
-            uint32_t cnt = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                pmb[k] = nl_colon_mask16(tb.v[k]);
-                cnt += __popc(pmb[k] & 0xFFFFu);
-            }
-            cnt = wave_add32(cnt);
-            if (lane == 0) sm.wave_cnt2[wave] = cnt;
-            wg_barrier();
-            if (tid == 0) {
-                uint32_t tc = 0;
-#pragma unroll
-                for (int w = 0; w < S::kWaves; ++w) tc += sm.wave_cnt2[w];
-                __hip_atomic_store(&p.status[p.b[b1].sbase + tb.t], mk_status(ep0, kFlagAgg, tc), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        const bool can_defer = has_b && !(ABL & ABL_MFMA_HASH) && !p.b[b0].hashes && p.dead <= (uint32_t)kOverlay;
-        const uint2 da = tile_lines<BLOCK, ABL>(p, sm, ta, ep0, g, can_defer ? rec_buf : nullptr);
-        if (has_b) tile_store_lds<BLOCK, ABL>(sm, tb, pmb);
-        flush_records<BLOCK>(p, ta, rec_buf, da, ep0);
-        if (has_b) tile_lines<BLOCK, ABL>(p, sm, tb, ep0, g);
+    const uint32_t bi = batch_of(p, cls, ci);
+    if (bi == kMaxBatches) {   // padding block of an unbalanced class
         if (tid == 0) arrive(p, blockIdx.x, ep0);
         return;
     }
-    if (!(ABL & ABL_PERSIST)) {   // one tile per workgroup
-        const uint32_t bi = batch_of(p, cls, ci);
-        if (bi == kMaxBatches) {   // padding block of an unbalanced class
-            if (tid == 0) arrive(p, blockIdx.x, ep0);
-            return;
-        }
-        TileIn in;
-        tile_issue<BLOCK, ABL>(p, bi, ci - p.b[bi].tile0, in, tid);
-        if (tid < kPowTable) (&sm.kp_lo[0])[tid] = p.kpow[tid];   // kp_lo | kp_hi | kinv are contiguous
-        if (tid < 68) {   // kmask[n][d]: bytes 4d .. 4d+3 of a mask keeping the first n bytes
-            const int n = tid >> 2, d = tid & 3, kb = min(max(n - 4 * d, 0), 4);
-            sm.kmask[n][d] = kb == 4 ? 0xFFFFFFFFu : ((1u << (8 * kb)) - 1u);
-        }
-        if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
-        tile_load_lds<BLOCK, ABL>(p, sm, in, ep0, g);
-        tile_lines<BLOCK, ABL>(p, sm, in, ep0, g);
-        if (tid == 0) arrive(p, blockIdx.x, ep0);
-        return;
-    }
-    // persistent: the workgroups of a class take its tiles in order from a shared counter (no
-    // rounds: a tile's predecessors were handed out before it). The next tile's loads are in flight
-    // while the current one's lines are routed, and its '\n' count is published straight after.
-    const uint32_t total = p.cls_tiles[cls];
-    uint32_t *const grab = &p.ctl->grab[cls][0];
-    if (tid < kPowTable) (&sm.kp_lo[0])[tid] = p.kpow[tid];
-    if (tid < 68) {
-        const int n = tid >> 2, d = tid & 3, kb = min(max(n - 4 * d, 0), 4);
-        sm.kmask[n][d] = kb == 4 ? 0xFFFFFFFFu : ((1u << (8 * kb)) - 1u);
-    }
+    TileIn in;
+    tile_issue<BLOCK, ABL>(p, bi, ci - p.b[bi].tile0, in, tid);
+    if (tid < S::kPowWords) (&sm.kp_lo[0])[tid] = p.kpow[tid];   // kp_lo | kp_hi | kp_inv are contiguous
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
-    if (tid == 0) sm.grab0 = atomicAdd(grab, 1u);
-    wg_barrier();
-    ci = sm.grab0;
-    TileIn cur, nxt;
-    uint32_t cn = total;
-    if (ci < total) {
-        const uint32_t bi = batch_of(p, cls, ci);
-        tile_issue<BLOCK, ABL>(p, bi, ci - p.b[bi].tile0, cur, tid);
-        if (tid == 0) sm.grab = atomicAdd(grab, 1u);
-        tile_load_lds<BLOCK, ABL>(p, sm, cur, ep0, p.b[cur.bi].sbase + cur.t);   // barrier inside
-        cn = sm.grab;
-    }
-    while (ci < total) {
-        if (cn < total) {
-            const uint32_t bn = batch_of(p, cls, cn);
-            tile_issue<BLOCK, ABL>(p, bn, cn - p.b[bn].tile0, nxt, tid);
-        }
-        uint32_t cnn = 0;
-        if (tid == 0 && cn < total) cnn = atomicAdd(grab, 1u);   // the tile after next
-        tile_lines<BLOCK, ABL>(p, sm, cur, ep0, p.b[cur.bi].sbase + cur.t);
-        if (tid == 0) sm.grab = cn < total ? cnn : total;
-        wg_barrier();   // every reader of the current tile's LDS is done; sm.grab written
-        if (cn < total) tile_load_lds<BLOCK, ABL>(p, sm, nxt, ep0, p.b[nxt.bi].sbase + nxt.t);
-        cur = nxt;
-        ci = cn;
-        cn = sm.grab;
-    }
+    uint64_t nlm, clm;
+    tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm);
+    tile_lines<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm);
     if (tid == 0) arrive(p, blockIdx.x, ep0);
 }
 

@@ -38,6 +38,43 @@ struct sr_ctx {
     uint64_t *d_owner_start;
 };
 
+// The product instantiation is ABL_NONE. SR_VARIANT in the environment selects one of a few
+// compiled-in variants instead, for same-box A/B measurements with bench.py:
+// v05 = the round-1 v0.5 components (hash, masks, scanner, late base read, sc1-only granules).
+static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream_t stream) {
+    static const int v = [] {
+        const char *e = getenv("SR_VARIANT");
+        if (!e || !*e) return 0;
+        if (!strcmp(e, "late_base")) return 1;
+        if (!strcmp(e, "old_scanner")) return 3;
+        if (!strcmp(e, "old_hash")) return 4;
+        if (!strcmp(e, "old_masks")) return 5;
+        if (!strcmp(e, "v05")) return 6;
+        if (!strcmp(e, "agent_granules")) return 11;
+        // upper bounds, not routing (records wrong or missing; line counts still exact)
+        if (!strcmp(e, "fake_base")) return 7;
+        if (!strcmp(e, "no_hash")) return 8;
+        if (!strcmp(e, "no_lines")) return 9;
+        if (!strcmp(e, "fake_base_no_hash")) return 10;
+        return 0;
+    }();
+    switch (v) {
+    case 1: return launch_route<kBlock, ABL_LATE_BASE>(ds, p, stream);
+    case 3: return launch_route<kBlock, ABL_OLD_SCANNER>(ds, p, stream);
+    case 4: return launch_route<kBlock, ABL_OLD_HASH>(ds, p, stream);
+    case 5: return launch_route<kBlock, ABL_OLD_MASKS>(ds, p, stream);
+    case 6:
+        return launch_route<kBlock, ABL_OLD_HASH | ABL_OLD_MASKS | ABL_OLD_SCANNER | ABL_LATE_BASE | ABL_AGENT_GRANULES>(
+            ds, p, stream);
+    case 11: return launch_route<kBlock, ABL_AGENT_GRANULES>(ds, p, stream);
+    case 7: return launch_route<kBlock, ABL_FAKE_BASE>(ds, p, stream);
+    case 8: return launch_route<kBlock, ABL_NO_HASH>(ds, p, stream);
+    case 9: return launch_route<kBlock, ABL_NO_LINES>(ds, p, stream);
+    case 10: return launch_route<kBlock, ABL_FAKE_BASE | ABL_NO_HASH>(ds, p, stream);
+    default: return launch_route<kBlock, ABL_NONE>(ds, p, stream);
+    }
+}
+
 extern "C" {
 
 size_t sr_frame_datagram(uint8_t *dst, const uint8_t *src, size_t len) {
@@ -130,7 +167,7 @@ int sr_route_device(sr_ctx *c, const uint8_t *d_bytes, size_t nbytes, sr_record 
     if (max_records && !d_out) return -EINVAL;
     (void)hipSetDevice(c->device);
     const RouteParams p = c->ds.params(d_bytes, nbytes, d_out, max_records, d_hashes, d_n_records);
-    return launch_route<kBlock, ABL_NONE>(c->ds, p, c->stream);
+    return launch_variant(c->ds, p, c->stream);
 }
 
 int sr_route_device_many(sr_ctx *c, const sr_batch *batches, size_t count) {
@@ -147,7 +184,7 @@ int sr_route_device_many(sr_ctx *c, const sr_batch *batches, size_t count) {
         for (size_t i = i0; i < count && i < i0 + kMaxBatches; ++i)
             DeviceState::add_batch(p, batches[i].d_bytes, batches[i].nbytes, batches[i].d_out, batches[i].max_records,
                                    batches[i].d_hashes, batches[i].d_n_records);
-        const int rc = launch_route<kBlock, ABL_NONE>(c->ds, p, c->stream);
+        const int rc = launch_variant(c->ds, p, c->stream);
         if (rc) return rc;
     }
     return 0;

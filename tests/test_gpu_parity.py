@@ -269,3 +269,57 @@ def test_device_many_splits_past_launch_limit(pkg, oracle):
             recs = d_out[i].cpu().numpy().view(pkg.RECORD_DTYPE)[:k]
             exp, _, en = oracle.route(p, 7)
             assert k == en and np.array_equal(recs, exp), f"batch {i}"
+
+
+# ---- the records-only path (no hashes requested): every tile but the last kSpillDist of each XCD
+# class spills its last window of records, and a later tile copies them into place ------------------
+
+def test_full_config_digests_records_only(pkg, router_factory):
+    for key, d in sorted(load_digests().items()):
+        s = pkg.gen_stream(d["nbytes"], d["line_lens"], seed=d["seed"], p_invalid=d["p_invalid"])
+        words = np.array([int(x, 16) for x in d["alive"]], dtype=np.uint64)
+        r = router_factory(d["n_downstreams"], alive=words)
+        for _ in range(2):   # twice: the spill slots then hold the previous launch's records
+            recs, hs, n = r.route(s.data)
+            assert hs is None and n == d["n_lines"], key
+            assert hashlib.sha256(recs.tobytes()).hexdigest() == d["sha256_records"], key
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_hostile_stream_records_only_spilled(pkg, oracle, router_factory, seed):
+    """Hostile datagrams over more than 2 x kSpillDist tiles (records only)."""
+    rng = random.Random(700 + seed)
+    n = rng.choice([1, 4, 64])
+    alive = [1 if rng.random() > 0.2 else 0 for _ in range(n)]
+    framed = pkg.frame_datagrams(_hostile_stream(900 + seed, 9_000_000))
+    r = router_factory(n, max_batch=16 << 20, alive=alive)
+    cr, _, cn = oracle.route(framed, n, alive)
+    for _ in range(2):
+        recs, _, k = r.route(framed)
+        assert k == cn
+        assert np.array_equal(recs, cr), f"seed {seed}"
+
+
+def test_device_many_records_only_spilled(pkg, oracle):
+    """16 batches of 4 MiB in one launch (XCD classes of 512 tiles: spills copied across batches),
+    records only, and short-line tiles with several windows."""
+    import torch
+
+    parts = [pkg.gen_stream(4 << 20, [[64], [256], [64, 256, 1024], [16, 24]][i % 4], seed=800 + i,
+                            p_invalid=0.05 * (i % 3)).data for i in range(16)]
+    with pkg.Router(16, 4 << 20) as r:
+        r.set_stream(torch.cuda.current_stream().cuda_stream)
+        d_in = [torch.from_numpy(p.copy()).to("cuda") for p in parts]
+        d_out = [torch.empty(int(p.size) * 8, dtype=torch.uint8, device="cuda") for p in parts]
+        d_n = torch.full((16,), -1, dtype=torch.int64, device="cuda")
+        descs = [(d_in[i].data_ptr(), int(p.size), d_out[i].data_ptr(), int(p.size), None, d_n.data_ptr() + 8 * i)
+                 for i, p in enumerate(parts)]
+        for _ in range(3):
+            r.route_device_many(descs)
+        torch.cuda.synchronize()
+        counts = d_n.cpu().numpy()
+        for i, p in enumerate(parts):
+            k = int(counts[i])
+            recs = d_out[i].cpu().numpy().view(pkg.RECORD_DTYPE)[:k]
+            exp, _, en = oracle.route(p, 16)
+            assert k == en and np.array_equal(recs, exp), f"batch {i}"

@@ -46,7 +46,7 @@ struct Ctx {
     DeviceState ds[kMaxS];
     std::vector<uint8_t *> batches;
     std::vector<size_t> sizes;
-    sr_record *d_out[kMaxS];
+    sr_record *d_out[kMaxS][16];
     uint64_t *d_n;
     size_t max_lines;
     uint32_t *sink;
@@ -68,7 +68,7 @@ float time_variant(Ctx &c, int S, int reps, int M = 1) {
             RouteParams p = c.ds[st].params();
             for (int m = 0; m < M; ++m) {
                 const int k = (i * M + m) % B;
-                DeviceState::add_batch(p, c.batches[k], c.sizes[k], c.d_out[st], c.max_lines, nullptr, c.d_n + k);
+                DeviceState::add_batch(p, c.batches[k], c.sizes[k], c.d_out[st][m % 16], c.max_lines, nullptr, c.d_n + k);
             }
             launch_route<BLOCK, V>(c.ds[st], p, c.s[st]);
         }
@@ -130,7 +130,8 @@ int main(int argc, char **argv) {
         lines.push_back(nl);
     }
     c.max_lines = lines[0];
-    for (int st = 0; st < kMaxS; ++st) CK(hipMalloc(&c.d_out[st], c.max_lines * sizeof(sr_record)));
+    for (int st = 0; st < kMaxS; ++st)
+        for (int m = 0; m < 16; ++m) CK(hipMalloc(&c.d_out[st][m], c.max_lines * sizeof(sr_record)));
     CK(hipMalloc(&c.d_n, B * sizeof(uint64_t)));
     CK(hipMalloc(&c.sink, 4));
 
@@ -146,10 +147,10 @@ int main(int argc, char **argv) {
             if (round == 0) rows.push_back(Row{name, {0, 0, 0}});
             rows[i++].us[round] = us;
         };
+        put("b256_m16_lds_pad", time_variant<256, ABL_LDS_PAD>(c, 1, reps, 16));
+        put("b256_m16_agent_granules", time_variant<256, ABL_AGENT_GRANULES>(c, 1, reps, 16));
         put("b256_m16_old_masks", time_variant<256, ABL_OLD_MASKS>(c, 1, reps, 16));
         put("b256_m16_old_scanner", time_variant<256, ABL_OLD_SCANNER>(c, 1, reps, 16));
-        put("b256_m16_pair", time_variant<256, ABL_PAIR>(c, 1, reps, 16));
-        put("b256_m16_pair_fake_base", time_variant<256, ABL_PAIR | ABL_FAKE_BASE>(c, 1, reps, 16));
         put("b256_m16_fake_base", time_variant<256, ABL_FAKE_BASE>(c, 1, reps, 16));
         put("b256_m16_fake_base_no_hash", time_variant<256, ABL_FAKE_BASE | ABL_NO_HASH>(c, 1, reps, 16));
         put("b256_m16_late_base", time_variant<256, ABL_LATE_BASE>(c, 1, reps, 16));
@@ -158,12 +159,6 @@ int main(int argc, char **argv) {
         put("b256_m16_no_hash_no_lookback", time_variant<256, ABL_NO_HASH | ABL_NO_LOOKBACK>(c, 1, reps, 16));
         put("b256_m16_no_xcd_local", time_variant<256, ABL_NO_XCD_LOCAL>(c, 1, reps, 16));
         put("b256_m16_no_hash_no_prologue", time_variant<256, ABL_NO_HASH | ABL_NO_PROLOGUE>(c, 1, reps, 16));
-        put("b256_m16_persist", time_variant<256, ABL_PERSIST>(c, 1, reps, 16));
-        put("b256_m16_persist_no_lookback", time_variant<256, ABL_PERSIST | ABL_NO_LOOKBACK>(c, 1, reps, 16));
-        put("b256_m16_persist_no_lookback_no_hash", time_variant<256, ABL_PERSIST | ABL_NO_LOOKBACK | ABL_NO_HASH>(c, 1, reps, 16));
-        put("b256_m16_persist_load_only", time_variant<256, ABL_PERSIST | ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps, 16));
-        put("b256_m16_persist_no_lines", time_variant<256, ABL_PERSIST | ABL_NO_LINES>(c, 1, reps, 16));
-        put("b256_m16_persist_no_hash", time_variant<256, ABL_PERSIST | ABL_NO_HASH>(c, 1, reps, 16));
         put("b512_m16", time_variant<512, ABL_NONE>(c, 1, reps, 16));
         put("b256_m16_no_hash", time_variant<256, ABL_NO_HASH>(c, 1, reps, 16));
         put("b512_m16_no_hash", time_variant<512, ABL_NO_HASH>(c, 1, reps, 16));
@@ -181,7 +176,7 @@ int main(int argc, char **argv) {
     // correctness: each product-shaped variant's line count on batch 0
     {
         uint64_t n = 0;
-        const RouteParams p = c.ds[0].params(c.batches[0], c.sizes[0], c.d_out[0], c.max_lines, nullptr, c.d_n);
+        const RouteParams p = c.ds[0].params(c.batches[0], c.sizes[0], c.d_out[0][0], c.max_lines, nullptr, c.d_n);
         launch_route<1024, ABL_NONE>(c.ds[0], p, c.s[0]);
         CK(hipMemcpyAsync(&n, c.d_n, 8, hipMemcpyDeviceToHost, c.s[0]));
         CK(hipStreamSynchronize(c.s[0]));
@@ -195,7 +190,7 @@ int main(int argc, char **argv) {
         std::vector<uint64_t> n(16);
         RouteParams p = c.ds[0].params();
         for (int k = 0; k < 16; ++k)
-            DeviceState::add_batch(p, c.batches[k], c.sizes[k], c.d_out[0], c.max_lines, nullptr, c.d_n + k);
+            DeviceState::add_batch(p, c.batches[k], c.sizes[k], c.d_out[0][0], c.max_lines, nullptr, c.d_n + k);
         CK(hipMemsetAsync(c.d_n, 0xFF, 16 * 8, c.s[0]));
         launch_route<512, ABL_NONE>(c.ds[0], p, c.s[0]);
         CK(hipMemcpyAsync(n.data(), c.d_n, 16 * 8, hipMemcpyDeviceToHost, c.s[0]));
@@ -203,20 +198,6 @@ int main(int argc, char **argv) {
         int bad = 0;
         for (int k = 0; k < 16; ++k) bad += n[k] != lines[k];
         fprintf(stderr, "b512 m16: %d of 16 batch counts wrong\n", bad);
-        CK(hipMemsetAsync(c.d_n, 0xFF, 16 * 8, c.s[0]));
-        launch_route<256, ABL_PERSIST>(c.ds[0], p, c.s[0]);
-        CK(hipMemcpyAsync(n.data(), c.d_n, 16 * 8, hipMemcpyDeviceToHost, c.s[0]));
-        CK(hipStreamSynchronize(c.s[0]));
-        bad = 0;
-        for (int k = 0; k < 16; ++k) bad += n[k] != lines[k];
-        fprintf(stderr, "b256 persist m16: %d of 16 batch counts wrong\n", bad);
-        CK(hipMemsetAsync(c.d_n, 0xFF, 16 * 8, c.s[0]));
-        launch_route<256, ABL_PAIR>(c.ds[0], p, c.s[0]);
-        CK(hipMemcpyAsync(n.data(), c.d_n, 16 * 8, hipMemcpyDeviceToHost, c.s[0]));
-        CK(hipStreamSynchronize(c.s[0]));
-        bad = 0;
-        for (int k = 0; k < 16; ++k) bad += n[k] != lines[k];
-        fprintf(stderr, "b256 pair m16: %d of 16 batch counts wrong\n", bad);
     }
     printf("{\"line_len\": %u, \"batch_bytes\": %zu, \"us_per_batch\": {", line_len, batch);
     for (size_t r = 0; r < rows.size(); ++r) {
