@@ -230,6 +230,16 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
         cls_tiles[d.cls] += d.ntiles;
     }
     if (sb > ds.max_tiles) return -EINVAL;
+    for (int c = 0; c < 8; ++c)
+        for (int k = 0; k < kPerClass; ++k) p.cls_tab[c][k] = ~0u;
+    {
+        int fill[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (uint32_t j = 0; j < p.nb; ++j) {   // j ascending = tile0 ascending within a class
+            const BatchDesc &d = p.b[j];
+            if (fill[d.cls] >= kPerClass || d.tile0 + d.ntiles >= (1u << 26)) return -EINVAL;
+            p.cls_tab[d.cls][fill[d.cls]++] = ((d.tile0 + d.ntiles) << 6) | j;
+        }
+    }
     uint32_t grid_tiles = cls_tiles[0];
     if (xl) {
         uint32_t mx = 0;

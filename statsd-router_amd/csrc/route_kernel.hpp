@@ -126,6 +126,7 @@ struct Control {
 // [tile0, tile0 + ntiles) of the grid belong to batch i, each batch with its own look-back chain
 // (status granules at the same grid indices) and its own records and line count.
 constexpr int kMaxBatches = 32;
+constexpr int kPerClass = 8;   // batches per XCD class: <= 4 with 8+ batches (XCD-local), <= 7 below
 struct BatchDesc {
     const uint8_t *bytes;
     sr_record *recs;
@@ -154,7 +155,10 @@ struct RouteParams {
     uint64_t *status;        // per-tile '\n' count granules {epoch, flag, count} (written by the tile)
     uint64_t *bases;         // per-tile first-record granules {epoch, flag, base} (written by the scanner)
     PendingLine *pending;
-    uint64_t *dbg;           // ABL_STAMPS builds only: 8 timestamps per tile
+    uint64_t *dbg;           // ABL_STAMPS builds only: 16 timestamp slots per tile
+    // per XCD class c, its batches in tile order: (class-local end tile << 6) | batch index;
+    // ~0u after the last (one scalar load finds a tile's batch)
+    uint32_t cls_tab[8][kPerClass];
     BatchDesc b[kMaxBatches];
 };
 
@@ -429,7 +433,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
 
 template <unsigned ABL>
 __device__ __forceinline__ void stamp(const RouteParams &p, int tid, uint32_t t, int slot) {
-    if ((ABL & ABL_STAMPS) && tid == 0) p.dbg[(size_t)t * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+    if ((ABL & ABL_STAMPS) && tid == 0) p.dbg[(size_t)t * 16 + slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 // Segmented "line state" scan element: [63:32] newline count, [31] lane range holds a '\n',
@@ -866,12 +870,17 @@ struct KernelTraits {
 // outstanding global loads (a persistent workgroup keeps the next tile's loads in flight across it).
 __device__ __forceinline__ void wg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// The batch of tile ci of XCD class cls (kMaxBatches if none): at most kMaxBatches scalar compares.
-__device__ __forceinline__ uint32_t batch_of(const RouteParams &p, uint32_t cls, uint32_t ci) {
-    uint32_t bi = kMaxBatches;
-    for (uint32_t k = 0; k < p.nb; ++k)
-        if (p.b[k].cls == cls && ci >= p.b[k].tile0 && ci < p.b[k].tile0 + p.b[k].ntiles) bi = k;
-    return bi;
+// The batch of tile ci of XCD class cls (>= kMaxBatches: a padding block) and the tile's index
+// in it, from one scalar load of the class's row of cls_tab (no chain of dependent loads before
+// the tile's own loads can issue).
+__device__ __forceinline__ uint32_t batch_of(const RouteParams &p, uint32_t cls, uint32_t ci, uint32_t &t) {
+    const uint32_t *row = p.cls_tab[cls];
+    uint32_t k = 0;   // batches of the class that end at or before ci (ends ascend, ~0u pads)
+#pragma unroll
+    for (int j = 0; j < kPerClass; ++j) k += ci >= (row[j] >> 6) ? 1u : 0u;
+    if (k >= kPerClass) return 63u;
+    t = ci - (k ? row[k - 1] >> 6 : 0u);
+    return row[k] & 63u;
 }
 
 // One tile's input as loaded into registers: thread tid holds the tile's bytes [64 tid, 64 tid + 64)
@@ -894,8 +903,6 @@ __device__ __forceinline__ void tile_issue(const RouteParams &p, uint32_t bi, ui
         __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
     in.bi = bi;
     in.t = t;
-    in.sx = (ABL & ABL_AGENT_GRANULES) ? 0ull
-                                       : __hip_atomic_load(&p.ctl->scan_xcc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     in.hv = make_uint4(0, 0, 0, 0);
     if (tid < kHalo / 16 && t > 0 && !(ABL & ABL_NO_PROLOGUE))   // zeros before the batch start
         in.hv = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, T0 - kHalo + tid * 16, 0, 0));
@@ -910,7 +917,7 @@ __device__ __forceinline__ void tile_issue(const RouteParams &p, uint32_t bi, ui
 // count published for the scanner.
 template <int BLOCK, unsigned ABL>
 __device__ __forceinline__ void tile_load(const RouteParams &p, SmemT<BLOCK> &sm, const TileIn &in, uint32_t epoch,
-                                          uint32_t g, uint64_t &nlm, uint64_t &clm) {
+                                          uint32_t g, uint64_t &nlm, uint64_t &clm, uint32_t &c_in) {
     using S = SmemT<BLOCK>;
     constexpr int kWaves = S::kWaves;
     constexpr int kHalo = S::kHalo;
@@ -939,8 +946,8 @@ __device__ __forceinline__ void tile_load(const RouteParams &p, SmemT<BLOCK> &sm
               __builtin_amdgcn_perm(m[1], m[0], 0x05040100u);
         clm = ((uint64_t)__builtin_amdgcn_perm(m[3], m[2], 0x07060302u) << 32) |
               __builtin_amdgcn_perm(m[1], m[0], 0x07060302u);
-        const uint32_t cnt = wave_add32((uint32_t)__popcll(nlm));
-        if (lane == 0) sm.wave_cnt[wave] = cnt;
+        c_in = wave_incl_add32((uint32_t)__popcll(nlm));   // also the line scan's '\n' count
+        if (lane == 63) sm.wave_cnt[wave] = c_in;
     }
     wg_barrier();
     stamp<ABL>(p, tid, g, 1);
@@ -959,7 +966,7 @@ __device__ __forceinline__ void tile_load(const RouteParams &p, SmemT<BLOCK> &sm
 // LDS image and whose chunk masks are in nlm / clm.
 template <int BLOCK, unsigned ABL>
 __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &sm, const TileIn &in, uint32_t epoch,
-                                           uint32_t g, uint64_t nlm, uint64_t clm) {
+                                           uint32_t g, uint64_t nlm, uint64_t clm, uint32_t c_in) {
     stamp<ABL>(p, threadIdx.x, g, 1);
     using S = SmemT<BLOCK>;
     constexpr int kWaves = S::kWaves;
@@ -1002,7 +1009,6 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
         }
         cand = cm ? (uint32_t)(o + __builtin_ctzll(cm)) : (uint32_t)kNone;
     }
-    const uint32_t c_in = wave_incl_add32((uint32_t)ncnt);
     const uint32_t l_in = wave_incl_max32(nlm ? (uint32_t)tid + 1u : 0u);
     const uint32_t k_in = wave_incl_min32(((uint32_t)(BLOCK - (int)l_in) << 17) | cand);
     if (lane == 63) *(uint4 *)&sm.wave_scan[wave][0] = make_uint4(c_in, l_in, k_in, 0u);
@@ -1235,25 +1241,40 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
         return;
     }
     const uint32_t g = blockIdx.x - p.nb;   // tile workgroup index within the launch
+    stamp<ABL>(p, tid, g, 8);
+    if ((ABL & ABL_STAMPS) && tid == 0) {   // placement: HW_ID (CU / SH / SE) and XCC_ID
+        uint32_t hw;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        p.dbg[(size_t)g * 16 + 10] = hw;
+        p.dbg[(size_t)g * 16 + 11] = xcc_id();
+    }
     // Launches of 8+ batches keep every batch on one XCD class (blocks b and b + 8 share an XCD):
     // a tile's predecessors then start before it on the same dispatcher, and its scanner (block
     // b, same class) sits beside them.
     const uint32_t cls = p.xcd_local ? (g & 7u) : 0u;
     uint32_t ci = p.xcd_local ? (g >> 3) : g;
-    const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t bi = batch_of(p, cls, ci);
-    if (bi == kMaxBatches) {   // padding block of an unbalanced class
-        if (tid == 0) arrive(p, blockIdx.x, ep0);
+    uint32_t t;
+    const uint32_t bi = batch_of(p, cls, ci, t);
+    if (bi >= kMaxBatches) {   // padding block of an unbalanced class
+        if (tid == 0) arrive(p, blockIdx.x, __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         return;
     }
+    // the tile's loads first; the epoch, the scanner's XCD and the power tables (needed only at
+    // the count publish and the hash) queue behind them
     TileIn in;
-    tile_issue<BLOCK, ABL>(p, bi, ci - p.b[bi].tile0, in, tid);
-    if (tid < S::kPowWords) (&sm.kp_lo[0])[tid] = p.kpow[tid];   // kp_lo | kp_hi | kp_inv are contiguous
+    tile_issue<BLOCK, ABL>(p, bi, t, in, tid);
+    const uint32_t kp = tid < S::kPowWords ? ((const uint32_t *)p.kpow)[tid] : 0u;
+    const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    in.sx = (ABL & ABL_AGENT_GRANULES) ? 0ull
+                                       : __hip_atomic_load(&p.ctl->scan_xcc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid < S::kPowWords) ((uint32_t *)&sm.kp_lo[0])[tid] = kp;   // kp_lo | kp_hi | kp_inv are contiguous
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
     uint64_t nlm, clm;
-    tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm);
-    tile_lines<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm);
+    uint32_t c_in;
+    tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
+    tile_lines<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
     if (tid == 0) arrive(p, blockIdx.x, ep0);
+    stamp<ABL>(p, tid, g, 9);
 }
 
 // Lines whose probe met more than kOverlay dead shards: run find_downstream (sr-main.c:86-117)

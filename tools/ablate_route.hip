@@ -157,7 +157,6 @@ int main(int argc, char **argv) {
         put("b256_m16_old_hash", time_variant<256, ABL_OLD_HASH>(c, 1, reps, 16));
         put("b256_m16_old_hash_no_lookback", time_variant<256, ABL_OLD_HASH | ABL_NO_LOOKBACK>(c, 1, reps, 16));
         put("b256_m16_no_hash_no_lookback", time_variant<256, ABL_NO_HASH | ABL_NO_LOOKBACK>(c, 1, reps, 16));
-        put("b256_m16_no_xcd_local", time_variant<256, ABL_NO_XCD_LOCAL>(c, 1, reps, 16));
         put("b256_m16_no_hash_no_prologue", time_variant<256, ABL_NO_HASH | ABL_NO_PROLOGUE>(c, 1, reps, 16));
         put("b512_m16", time_variant<512, ABL_NONE>(c, 1, reps, 16));
         put("b256_m16_no_hash", time_variant<256, ABL_NO_HASH>(c, 1, reps, 16));

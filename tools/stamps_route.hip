@@ -30,54 +30,6 @@ static double med(std::vector<double> v) {
     return v[v.size() / 2];
 }
 
-template <int BLOCK>
-void run(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size_t> &sizes, sr_record *d_out,
-         size_t max_lines, uint64_t *d_n, uint64_t *d_dbg, hipStream_t s, uint32_t line_len) {
-    const int L = (int)batches.size();
-    const uint32_t T = BLOCK * kLaneBytes;
-    const uint32_t ntiles = (uint32_t)((sizes[0] + T - 1) / T);
-    std::vector<uint64_t> h((size_t)L * ntiles * 8);
-    for (int w = 0; w < 4; ++w) {   // warm
-        RouteParams p = ds.params(batches[w], sizes[w], d_out, max_lines, nullptr, d_n);
-        p.dbg = d_dbg;
-        launch_route<BLOCK, ABL_STAMPS>(ds, p, s);
-    }
-    CK(hipStreamSynchronize(s));
-    for (int i = 0; i < L; ++i) {
-        RouteParams p = ds.params(batches[i], sizes[i], d_out, max_lines, nullptr, d_n);
-        p.dbg = d_dbg + (size_t)i * ntiles * 8;
-        launch_route<BLOCK, ABL_STAMPS>(ds, p, s);
-    }
-    CK(hipStreamSynchronize(s));
-    CK(hipMemcpy(h.data(), d_dbg, h.size() * 8, hipMemcpyDeviceToHost));
-    std::vector<double> span, start_spread, end_spread, ph[6];
-    for (int i = 0; i < L; ++i) {
-        const uint64_t *d = h.data() + (size_t)i * ntiles * 8;
-        uint64_t s0 = ~0ull, s0max = 0, e0 = ~0ull, e1 = 0;
-        for (uint32_t b = 0; b < ntiles; ++b) {
-            s0 = std::min(s0, d[b * 8 + 0]);
-            s0max = std::max(s0max, d[b * 8 + 0]);
-            e0 = std::min(e0, d[b * 8 + 6]);
-            e1 = std::max(e1, d[b * 8 + 6]);
-            const double u = 0.01;   // us per tick
-            ph[0].push_back((d[b * 8 + 1] - d[b * 8 + 0]) * u);   // loads -> LDS
-            ph[1].push_back((d[b * 8 + 2] - d[b * 8 + 1]) * u);   // masks + scan
-            ph[2].push_back((d[b * 8 + 3] - d[b * 8 + 2]) * u);   // look-back (wave 0)
-            ph[3].push_back((d[b * 8 + 4] - d[b * 8 + 2]) * u);   // to staged lines
-            ph[4].push_back((d[b * 8 + 5] - d[b * 8 + 4]) * u);   // hash + records
-            ph[5].push_back((d[b * 8 + 6] - d[b * 8 + 0]) * u);   // workgroup lifetime
-        }
-        span.push_back((e1 - s0) * 0.01);
-        start_spread.push_back((s0max - s0) * 0.01);
-        end_spread.push_back((e1 - e0) * 0.01);
-    }
-    printf("{\"block\": %d, \"line_len\": %u, \"tiles\": %u, \"span_us\": %.2f, \"start_spread_us\": %.2f, "
-           "\"end_spread_us\": %.2f, \"median_us\": {\"load\": %.2f, \"masks_scan\": %.2f, \"lookback\": %.2f, "
-           "\"to_staged\": %.2f, \"hash_records\": %.2f, \"lifetime\": %.2f}}\n",
-           BLOCK, line_len, ntiles, med(span), med(start_spread), med(end_spread), med(ph[0]), med(ph[1]), med(ph[2]),
-           med(ph[3]), med(ph[4]), med(ph[5]));
-}
-
 // one launch over all L batches (the product's multi-batch mode): per-phase medians over every
 // workgroup of the launch, plus the launch span
 template <int BLOCK>
@@ -87,7 +39,7 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
     const uint32_t T = BLOCK * kLaneBytes;
     uint32_t total = 0;
     for (int i = 0; i < L; ++i) total += (uint32_t)((sizes[i] + T - 1) / T);
-    std::vector<uint64_t> h((size_t)total * 8);
+    std::vector<uint64_t> h((size_t)total * 16);
     auto launch = [&]() {
         RouteParams p = ds.params();
         for (int i = 0; i < L; ++i)
@@ -97,7 +49,8 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
     };
     for (int w = 0; w < 3; ++w) launch();
     CK(hipStreamSynchronize(s));
-    CK(hipMemset(d_dbg, 0, h.size() * 8));
+    CK(hipMemsetAsync(d_dbg, 0, h.size() * 8, s));
+    CK(hipStreamSynchronize(s));
     launch();
     CK(hipStreamSynchronize(s));
     CK(hipMemcpy(h.data(), d_dbg, h.size() * 8, hipMemcpyDeviceToHost));
@@ -119,7 +72,7 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
         for (int j = 0; j < L; ++j) {
             uint64_t m = 0;
             for (size_t t = 0; t < order[j].size(); ++t) {
-                const uint64_t *d = h.data() + (size_t)order[j][t] * 8;
+                const uint64_t *d = h.data() + (size_t)order[j][t] * 16;
                 ++n;
                 if (d[3]) {
                     ++waited;
@@ -137,10 +90,42 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
                n, waited, pc(late, 0.1), pc(late, 0.5), pc(late, 0.9), pc(late, 0.99), pc(lag, 0.1), pc(lag, 0.5),
                pc(lag, 0.9), pc(lag, 0.99));
     }
-    std::vector<double> ph[6];
+    {   // raw per-tile dump for offline analysis: entry, stamp0, end, exit, hw_id, xcc
+        FILE *f = fopen("gpurun_out/stamps_raw.bin", "wb");
+        if (f) {
+            for (uint32_t t = 0; t < total; ++t) {
+                const uint64_t *d = h.data() + (size_t)t * 16;
+                const uint64_t r[8] = {d[8], d[0], d[6], d[9], d[10], d[11], d[3], d[7]};
+                fwrite(r, 8, 8, f);
+            }
+            fclose(f);
+        }
+    }
+    std::vector<double> ph[8];
     uint64_t s0 = ~0ull, e1 = 0;
+    {   // residency: tiles alive over the launch (start stamp 0 .. end stamp 6), in 1 us bins
+        std::vector<std::pair<uint64_t, uint64_t>> iv;
+        for (uint32_t b = 0; b < total; ++b) {
+            const uint64_t *d = h.data() + (size_t)b * 16;
+            if (d[8] && d[9]) iv.push_back({d[8], d[9]});   // kernel entry .. after arrive
+        }
+        uint64_t a = ~0ull, z = 0;
+        double busy = 0;
+        for (auto &x : iv) a = std::min(a, x.first), z = std::max(z, x.second), busy += (double)(x.second - x.first);
+        const int nb = (int)((z - a) / 100) + 1;
+        std::vector<double> occ(nb, 0.0), starts(nb, 0.0);
+        for (auto &x : iv) {
+            starts[(x.first - a) / 100] += 1;
+            for (uint64_t t = x.first; t < x.second; t += 10) occ[(t - a) / 100] += 0.1;
+        }
+        printf("{\"residency\": {\"span_us\": %.2f, \"mean_resident_tiles\": %.1f, \"per_us\": [", (z - a) * 0.01,
+               busy / (double)(z - a));
+        for (int i = 0; i < nb; ++i) printf("%s[%.0f, %.0f]", i ? ", " : "", occ[i], starts[i]);
+        printf("]}}\n");
+    }
     for (uint32_t b = 0; b < total; ++b) {
-        const uint64_t *d = h.data() + (size_t)b * 8;
+        const uint64_t *d = h.data() + (size_t)b * 16;
+        if (!d[0]) continue;
         s0 = std::min(s0, d[0]);
         e1 = std::max(e1, d[6]);
         const double u = 0.01;
@@ -150,6 +135,8 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
         ph[3].push_back((d[4] - d[2]) * u);
         ph[4].push_back((d[5] - d[4]) * u);
         ph[5].push_back((d[6] - d[0]) * u);
+        ph[6].push_back((d[0] - d[8]) * u);   // entry: epoch, batch lookup, load issue
+        ph[7].push_back((d[9] - d[8]) * u);   // entry .. after arrive
     }
     {
         std::vector<double> w = ph[2];
@@ -160,9 +147,9 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
     }
     printf("{\"mode\": \"%d batches per launch\", \"block\": %d, \"line_len\": %u, \"tiles\": %u, \"span_us\": %.2f, "
            "\"median_us\": {\"load\": %.2f, \"masks_scan\": %.2f, \"base_wait\": %.2f, \"to_staged\": %.2f, "
-           "\"hash_records\": %.2f, \"lifetime\": %.2f}}\n",
+           "\"hash_records\": %.2f, \"lifetime\": %.2f, \"entry\": %.2f, \"entry_to_exit\": %.2f}}\n",
            L, BLOCK, line_len, total, (e1 - s0) * 0.01, med(ph[0]), med(ph[1]), med(ph[2]), med(ph[3]), med(ph[4]),
-           med(ph[5]));
+           med(ph[5]), med(ph[6]), med(ph[7]));
 }
 
 int main(int argc, char **argv) {
@@ -189,7 +176,7 @@ int main(int argc, char **argv) {
     uint64_t *d_n, *d_dbg;
     CK(hipMalloc(&d_out, (size_t)L * nl * sizeof(sr_record)));
     CK(hipMalloc(&d_n, 8 * L));
-    CK(hipMalloc(&d_dbg, (size_t)L * 4096 * 8 * 8));
+    CK(hipMalloc(&d_dbg, (size_t)L * 4096 * 16 * 8));
     hipStream_t s;
     CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     run_many<256>(ds, batches, sizes, d_out, nl, d_n, d_dbg, s, line_len);
