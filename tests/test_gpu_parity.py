@@ -271,23 +271,22 @@ def test_device_many_splits_past_launch_limit(pkg, oracle):
             assert k == en and np.array_equal(recs, exp), f"batch {i}"
 
 
-# ---- the records-only path (no hashes requested): every tile but the last kSpillDist of each XCD
-# class spills its last window of records, and a later tile copies them into place ------------------
+# ---- the records-only path (no hashes requested), over many tiles and repeated launches ----------
 
 def test_full_config_digests_records_only(pkg, router_factory):
     for key, d in sorted(load_digests().items()):
         s = pkg.gen_stream(d["nbytes"], d["line_lens"], seed=d["seed"], p_invalid=d["p_invalid"])
         words = np.array([int(x, 16) for x in d["alive"]], dtype=np.uint64)
         r = router_factory(d["n_downstreams"], alive=words)
-        for _ in range(2):   # twice: the spill slots then hold the previous launch's records
+        for _ in range(2):   # twice: the granules then hold the previous launch's epoch
             recs, hs, n = r.route(s.data)
             assert hs is None and n == d["n_lines"], key
             assert hashlib.sha256(recs.tobytes()).hexdigest() == d["sha256_records"], key
 
 
 @pytest.mark.parametrize("seed", range(3))
-def test_hostile_stream_records_only_spilled(pkg, oracle, router_factory, seed):
-    """Hostile datagrams over more than 2 x kSpillDist tiles (records only)."""
+def test_hostile_stream_records_only(pkg, oracle, router_factory, seed):
+    """Hostile datagrams over ~550 tiles (records only)."""
     rng = random.Random(700 + seed)
     n = rng.choice([1, 4, 64])
     alive = [1 if rng.random() > 0.2 else 0 for _ in range(n)]
@@ -300,9 +299,9 @@ def test_hostile_stream_records_only_spilled(pkg, oracle, router_factory, seed):
         assert np.array_equal(recs, cr), f"seed {seed}"
 
 
-def test_device_many_records_only_spilled(pkg, oracle):
-    """16 batches of 4 MiB in one launch (XCD classes of 512 tiles: spills copied across batches),
-    records only, and short-line tiles with several windows."""
+def test_device_many_records_only(pkg, oracle):
+    """16 batches of 4 MiB in one launch (two batches per XCD class), records only, and short-line
+    tiles with several windows."""
     import torch
 
     parts = [pkg.gen_stream(4 << 20, [[64], [256], [64, 256, 1024], [16, 24]][i % 4], seed=800 + i,
