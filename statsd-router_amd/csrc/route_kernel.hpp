@@ -75,6 +75,7 @@ enum : unsigned {
     ABL_FAKE_BASE = 4096u,  // ablation: base = t * (this tile's count), exact only for uniform tiles (C2)
     ABL_LATE_BASE = 2048u,  // read the record base only after hashing (round-1 v0.5)
     ABL_AGENT_GRANULES = 262144u,  // every count / base granule stored sc1 (round-1 v0.5), whatever the XCDs
+    ABL_SCAN_SERIAL = 524288u,  // round-1 v0.6 scanner: 256 granules per round trip, one poll in flight
     ABL_OLD_HASH = 1024u,   // round-1 v0.5 per-segment sdbm (v_alignbyte reads, compiler-extracted bytes)
 };
 
@@ -721,7 +722,12 @@ __device__ void scan_batch(const RouteParams &p, const BatchDesc &bd, uint32_t e
 // poll. Wave 0 polls the tiles' counts and computes their bases into an LDS ring (head index
 // released after the writes); wave 1 publishes the ring to the bases granules and the batch's
 // line count. Flow control keeps the ring (the LDS image, 4096 entries) from overrunning.
-template <int BLOCK, bool kAgentOnly>
+// ABL_STAMPS: tile workgroup index (the dbg slot) of tile t of batch bd
+__device__ __forceinline__ uint32_t stamp_block(const RouteParams &p, const BatchDesc &bd, uint32_t t) {
+    return p.xcd_local ? (bd.tile0 + t) * 8u + bd.cls : bd.tile0 + t;
+}
+
+template <int BLOCK, unsigned ABL>
 __device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint32_t epoch, SmemT<BLOCK> &sm,
                                  int wave, int lane) {
     constexpr uint32_t kRing = 4096;
@@ -734,12 +740,87 @@ __device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint
             __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
         const uint32_t ep = epoch & 0x3FFFFFFFu;
         // tiles that share this XCD get their base by a plain store (ring entry bit 31)
+        constexpr bool kAgentOnly = (ABL & ABL_AGENT_GRANULES) != 0;
         const uint32_t mine = kAgentOnly ? 0u : (8u | xcc_id()) << 28;
         if (lane == 0 && !kAgentOnly)
             __hip_atomic_store(&p.ctl->scan_xcc[blockIdx.x], mk_status(epoch, kFlagXcc, xcc_id()), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-        uint32_t run = 0, c = 0;
+        uint32_t run = 0, c = 0, rounds = 0;
         int spin = 0;
+        if (!(ABL & ABL_SCAN_SERIAL)) {
+            // Pipelined polls of the 64 granules from c: the next poll is issued before the previous
+            // one is consumed, so two are in flight and the scanner looks every half round trip
+            // (a poll's round trip under the tiles' load is ~1.2 us). Unrolled by two with the
+            // roles of the two poll registers swapped, so no copy waits for a poll in flight.
+            const uint32_t last = bd.ntiles - 1u;
+            auto poll = [&](uint32_t c0) -> uint64_t {   // unconditional load: clamped address
+                const uint32_t tt = c0 + lane < last ? c0 + lane : last;
+                return __hip_atomic_load(&status[tt], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            };
+            // consume poll `cur` (tiles [ccur, ccur + 64)) from c, with poll `nxt` issued first
+            auto step = [&](uint64_t cur, uint32_t ccur, uint64_t &nxt, uint32_t &cnxt) {
+                while (c + 64 > __hip_atomic_load(&sm.scan_pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) + kRing)
+                    __builtin_amdgcn_s_sleep(1);
+                cnxt = c;
+                nxt = poll(c);
+                const int sh = (int)(c - ccur);
+                uint64_t st = cur;
+                if (sh) {
+                    const int src = (lane + sh) & 63;
+                    st = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(cur >> 32), src) << 32) |
+                         (uint32_t)__shfl((int)(uint32_t)cur, src);
+                }
+                const uint32_t tt = c + lane;
+                uint32_t cnt = 0, loc = 0;
+                bool have = tt >= bd.ntiles;
+                if (!have && lane + sh < 64 && granule_ok(st, ep, kFlagAgg)) {
+                    cnt = (uint32_t)st & kCountMask;
+                    loc = ((uint32_t)st & ~kCountMask) == mine && mine ? 0x80000000u : 0u;
+                    have = true;
+                }
+                if (spin >= kSpinBudget) {   // still incomplete: count the silent tiles here
+                    uint64_t missing = __ballot(!have);
+                    while (missing) {
+                        const int L = __builtin_ctzll(missing);
+                        missing &= missing - 1;
+                        const uint32_t c2 = count_tile_wave<BLOCK>(bd.nbytes, rsrc, c + (uint32_t)L, lane);
+                        if (lane == L) {
+                            cnt = c2;
+                            have = true;
+                        }
+                    }
+                }
+                const uint64_t missing = __ballot(!have);
+                const int nready = missing ? __builtin_ctzll(missing) : 64;
+                if (nready) {
+                    const uint32_t v = lane < nready ? cnt : 0u;
+                    const uint32_t incl = wave_incl_add32(v);
+                    if (lane < nready && tt < bd.ntiles) {
+                        ring[tt % kRing] = (run + incl - v) | loc;
+                        if (ABL & ABL_STAMPS)
+                            p.dbg[(size_t)stamp_block(p, bd, tt) * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+                    }
+                    run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                    c += (uint32_t)nready;
+                    if (c > bd.ntiles) c = bd.ntiles;
+                    spin = 0;
+                    if (lane == 0) {
+                        if (c >= bd.ntiles) sm.scan_total = run;
+                        __hip_atomic_store(&sm.scan_head, c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                } else {
+                    ++spin;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            };
+            uint64_t pa = poll(0), pb = 0;
+            uint32_t ca = 0, cb = 0;
+            while (c < bd.ntiles) {
+                step(pa, ca, pb, cb);
+                if (c >= bd.ntiles) break;
+                step(pb, cb, pa, ca);
+            }
+        }
         while (c < bd.ntiles) {
             // the publisher must have taken the ring slots this round may overwrite
             while (c + 64 * kGroups > __hip_atomic_load(&sm.scan_pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) +
@@ -747,6 +828,7 @@ __device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint
                 __builtin_amdgcn_s_sleep(1);
             uint32_t cnt[kGroups], loc[kGroups];
             bool have[kGroups];
+            const uint64_t t_iss = (ABL & ABL_STAMPS) ? __builtin_amdgcn_s_memrealtime() : 0;
 #pragma unroll
             for (int k = 0; k < kGroups; ++k) {
                 const uint32_t tt = c + 64 * k + lane;
@@ -761,6 +843,14 @@ __device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint
                         have[k] = true;
                     }
                 }
+            }
+            if (ABL & ABL_STAMPS) {   // poll round trips: (issue, all returned) per round
+                if (lane == 0) {
+                    const size_t o = 300000u + blockIdx.x * 4096u + (rounds & 2047u) * 2u;
+                    p.dbg[o] = t_iss;
+                    p.dbg[o + 1] = __builtin_amdgcn_s_memrealtime();
+                }
+                ++rounds;
             }
             if (spin >= kSpinBudget) {   // head group still incomplete: count its silent tiles here
                 uint64_t missing = __ballot(!have[0]);
@@ -782,7 +872,10 @@ __device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint
                 if (nready == 0) break;
                 const uint32_t v = lane < nready ? cnt[k] : 0u;
                 const uint32_t incl = wave_incl_add32(v);
-                if (lane < nready && c + lane < bd.ntiles) ring[(c + lane) % kRing] = (run + incl - v) | loc[k];
+                if (lane < nready && c + lane < bd.ntiles) {
+                    ring[(c + lane) % kRing] = (run + incl - v) | loc[k];
+                    if (ABL & ABL_STAMPS) p.dbg[(size_t)stamp_block(p, bd, c + lane) * 16 + 13] = __builtin_amdgcn_s_memrealtime();
+                }
                 run += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                 c += (uint32_t)nready;
                 if (nready < 64 || c >= bd.ntiles) break;
@@ -811,6 +904,7 @@ __device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint
             for (uint32_t i = pub + lane; i < h; i += 64) {
                 const uint32_t r = ring[i % kRing];
                 granule_store(&bases[i], mk_status(epoch, kFlagBase, r & 0x7FFFFFFFu), (r >> 31) != 0u);
+                if (ABL & ABL_STAMPS) p.dbg[(size_t)stamp_block(p, bd, i) * 16 + 12] = __builtin_amdgcn_s_memrealtime();
             }
             pub = h;
             if (lane == 0) __hip_atomic_store(&sm.scan_pub, pub, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1235,7 +1329,7 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
                 sm.scan_total = 0;
             }
             wg_barrier();
-            scan_batch_split<BLOCK, (ABL & ABL_AGENT_GRANULES) != 0>(p, p.b[blockIdx.x], ep0, sm, wave, lane);
+            scan_batch_split<BLOCK, ABL>(p, p.b[blockIdx.x], ep0, sm, wave, lane);
             if (tid == 64) arrive(p, blockIdx.x, ep0);   // the publisher, after its last store
         }
         return;

@@ -51,6 +51,7 @@ static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream
         if (!strcmp(e, "old_masks")) return 5;
         if (!strcmp(e, "v05")) return 6;
         if (!strcmp(e, "agent_granules")) return 11;
+        if (!strcmp(e, "scan_serial")) return 12;
         // upper bounds, not routing (records wrong or missing; line counts still exact)
         if (!strcmp(e, "fake_base")) return 7;
         if (!strcmp(e, "no_hash")) return 8;
@@ -67,6 +68,7 @@ static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream
         return launch_route<kBlock, ABL_OLD_HASH | ABL_OLD_MASKS | ABL_OLD_SCANNER | ABL_LATE_BASE | ABL_AGENT_GRANULES>(
             ds, p, stream);
     case 11: return launch_route<kBlock, ABL_AGENT_GRANULES>(ds, p, stream);
+    case 12: return launch_route<kBlock, ABL_SCAN_SERIAL>(ds, p, stream);
     case 7: return launch_route<kBlock, ABL_FAKE_BASE>(ds, p, stream);
     case 8: return launch_route<kBlock, ABL_NO_HASH>(ds, p, stream);
     case 9: return launch_route<kBlock, ABL_NO_LINES>(ds, p, stream);

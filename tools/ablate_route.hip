@@ -148,6 +148,7 @@ int main(int argc, char **argv) {
             rows[i++].us[round] = us;
         };
         put("b256_m16_lds_pad", time_variant<256, ABL_LDS_PAD>(c, 1, reps, 16));
+        put("b256_m16_scan_serial", time_variant<256, ABL_SCAN_SERIAL>(c, 1, reps, 16));
         put("b256_m16_agent_granules", time_variant<256, ABL_AGENT_GRANULES>(c, 1, reps, 16));
         put("b256_m16_old_masks", time_variant<256, ABL_OLD_MASKS>(c, 1, reps, 16));
         put("b256_m16_old_scanner", time_variant<256, ABL_OLD_SCANNER>(c, 1, reps, 16));

@@ -49,7 +49,7 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
     };
     for (int w = 0; w < 3; ++w) launch();
     CK(hipStreamSynchronize(s));
-    CK(hipMemsetAsync(d_dbg, 0, h.size() * 8, s));
+    CK(hipMemsetAsync(d_dbg, 0, (size_t)16 * 4096 * 16 * 8, s));
     CK(hipStreamSynchronize(s));
     launch();
     CK(hipStreamSynchronize(s));
@@ -95,11 +95,26 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
         if (f) {
             for (uint32_t t = 0; t < total; ++t) {
                 const uint64_t *d = h.data() + (size_t)t * 16;
-                const uint64_t r[8] = {d[8], d[0], d[6], d[9], d[10], d[11], d[3], d[7]};
-                fwrite(r, 8, 8, f);
+                const uint64_t r[12] = {d[8], d[0], d[6], d[9], d[10], d[11], d[3], d[7], d[1], d[13], d[12], d[4]};
+                fwrite(r, 8, 12, f);
             }
             fclose(f);
         }
+    }
+    {   // scanner poll rounds (batch 0 and 8): round-trip percentiles and round count
+        std::vector<uint64_t> sc(16 * 4096);
+        CK(hipMemcpy(sc.data(), d_dbg + 300000, 16 * 4096 * 8, hipMemcpyDeviceToHost));
+        std::vector<double> rt;
+        int nr = 0;
+        for (int b = 0; b < 16; ++b)
+            for (int r = 0; r < 2048; ++r) {
+                const uint64_t a = sc[b * 4096 + 2 * r], z = sc[b * 4096 + 2 * r + 1];
+                if (a && z) rt.push_back((double)(z - a) * 0.01), ++nr;
+            }
+        std::sort(rt.begin(), rt.end());
+        if (!rt.empty())
+            printf("{\"scanner_poll_rt_us\": [%.2f, %.2f, %.2f, %.2f], \"rounds_per_batch\": %.1f}\n", rt[rt.size() / 10],
+                   rt[rt.size() / 2], rt[rt.size() * 9 / 10], rt[rt.size() * 99 / 100], nr / 16.0);
     }
     std::vector<double> ph[8];
     uint64_t s0 = ~0ull, e1 = 0;
