@@ -73,7 +73,8 @@ enum : unsigned {
     ABL_OLD_MASKS = 65536u,  // round-1 v0.5 piece masks (one SWAR test per pattern)
     ABL_OLD_SCANNER = 32768u, // round-1 v0.5 scanner: one wave polls and publishes
     ABL_FAKE_BASE = 4096u,  // ablation: base = t * (this tile's count), exact only for uniform tiles (C2)
-    ABL_LATE_BASE = 2048u,  // read the record base only after hashing (round-1 v0.5)
+    ABL_EARLY_BASE = 2048u,  // also read the record base when staging ends (round-1 v0.6a/b; no gain once
+                             // the pipelined scanner publishes ahead of need)
     ABL_AGENT_GRANULES = 262144u,  // every count / base granule stored sc1 (round-1 v0.5), whatever the XCDs
     ABL_SCAN_SERIAL = 524288u,  // round-1 v0.6 scanner: 256 granules per round trip, one poll in flight
     ABL_OLD_HASH = 1024u,   // round-1 v0.5 per-segment sdbm (v_alignbyte reads, compiler-extracted bytes)
@@ -579,8 +580,12 @@ __device__ __forceinline__ uint64_t sdbm_img(const S &sm, int a, int n) {
     if (F == 0) return sdbm_dword_fast(0, first & ((1u << (8 * rem)) - 1u)) * sm.kp_inv[4 - rem];
     uint64_t h = sdbm_dword_fast(0, first);
     int m = 1;
-    for (; m < F && m < cross; ++m) h = sdbm_dword_fast(h, p[m]);
-    for (; m < F; ++m) h = sdbm_dword_fast(h, p[m + 1]);
+    // two dwords per iteration (half the loop control; adjacent reads pair into ds_read2)
+    const int F1 = F < cross ? F : cross;   // dwords before the row's pad dword
+    for (; m + 1 < F1; m += 2) h = sdbm_dword_fast(sdbm_dword_fast(h, p[m]), p[m + 1]);
+    if (m < F1) h = sdbm_dword_fast(h, p[m++]);
+    for (; m + 1 < F; m += 2) h = sdbm_dword_fast(sdbm_dword_fast(h, p[m + 1]), p[m + 2]);
+    if (m < F) h = sdbm_dword_fast(h, p[1 + m++]);
     if (rem) h = sdbm_dword_fast(h, p[m + (m >= cross ? 1 : 0)] & ((1u << (8 * rem)) - 1u)) * sm.kp_inv[4 - rem];
     return h;
 }
@@ -1225,10 +1230,10 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
         }
         wg_barrier();
         if (wbase == 0) stamp<ABL>(p, tid, g, 4);
-        // the tile's record base, read ahead: the load's round trip overlaps the hashing, and the
-        // granule is re-polled at record time only if the scanner had not yet published it
+        // the tile's record base is read when the first record is written (ABL_EARLY_BASE: also
+        // here); the pipelined scanner has normally published it well before
         uint64_t st_early = 0;
-        if (!have_base && !(ABL & ABL_LATE_BASE))
+        if (!have_base && (ABL & ABL_EARLY_BASE))
             st_early = __hip_atomic_load(base_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (!(ABL & ABL_NO_LINES)) {
             const int s_pre = sm.s_pre;

@@ -40,12 +40,12 @@ struct sr_ctx {
 
 // The product instantiation is ABL_NONE. SR_VARIANT in the environment selects one of a few
 // compiled-in variants instead, for same-box A/B measurements with bench.py:
-// v05 = the round-1 v0.5 components (hash, masks, scanner, late base read, sc1-only granules).
+// v05 = the round-1 v0.5 components (hash, masks, serial scanner, late base read, sc1-only granules).
 static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream_t stream) {
     static const int v = [] {
         const char *e = getenv("SR_VARIANT");
         if (!e || !*e) return 0;
-        if (!strcmp(e, "late_base")) return 1;
+        if (!strcmp(e, "early_base")) return 1;
         if (!strcmp(e, "old_scanner")) return 3;
         if (!strcmp(e, "old_hash")) return 4;
         if (!strcmp(e, "old_masks")) return 5;
@@ -60,12 +60,12 @@ static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream
         return 0;
     }();
     switch (v) {
-    case 1: return launch_route<kBlock, ABL_LATE_BASE>(ds, p, stream);
+    case 1: return launch_route<kBlock, ABL_EARLY_BASE>(ds, p, stream);
     case 3: return launch_route<kBlock, ABL_OLD_SCANNER>(ds, p, stream);
     case 4: return launch_route<kBlock, ABL_OLD_HASH>(ds, p, stream);
     case 5: return launch_route<kBlock, ABL_OLD_MASKS>(ds, p, stream);
     case 6:
-        return launch_route<kBlock, ABL_OLD_HASH | ABL_OLD_MASKS | ABL_OLD_SCANNER | ABL_LATE_BASE | ABL_AGENT_GRANULES>(
+        return launch_route<kBlock, ABL_OLD_HASH | ABL_OLD_MASKS | ABL_OLD_SCANNER | ABL_AGENT_GRANULES | ABL_SCAN_SERIAL>(
             ds, p, stream);
     case 11: return launch_route<kBlock, ABL_AGENT_GRANULES>(ds, p, stream);
     case 12: return launch_route<kBlock, ABL_SCAN_SERIAL>(ds, p, stream);

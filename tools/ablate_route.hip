@@ -154,7 +154,7 @@ int main(int argc, char **argv) {
         put("b256_m16_old_scanner", time_variant<256, ABL_OLD_SCANNER>(c, 1, reps, 16));
         put("b256_m16_fake_base", time_variant<256, ABL_FAKE_BASE>(c, 1, reps, 16));
         put("b256_m16_fake_base_no_hash", time_variant<256, ABL_FAKE_BASE | ABL_NO_HASH>(c, 1, reps, 16));
-        put("b256_m16_late_base", time_variant<256, ABL_LATE_BASE>(c, 1, reps, 16));
+        put("b256_m16_early_base", time_variant<256, ABL_EARLY_BASE>(c, 1, reps, 16));
         put("b256_m16_old_hash", time_variant<256, ABL_OLD_HASH>(c, 1, reps, 16));
         put("b256_m16_old_hash_no_lookback", time_variant<256, ABL_OLD_HASH | ABL_NO_LOOKBACK>(c, 1, reps, 16));
         put("b256_m16_no_hash_no_lookback", time_variant<256, ABL_NO_HASH | ABL_NO_LOOKBACK>(c, 1, reps, 16));
