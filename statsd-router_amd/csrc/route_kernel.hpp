@@ -582,10 +582,12 @@ __device__ __forceinline__ uint64_t sdbm_img(const S &sm, int a, int n) {
     int m = 1;
     // two dwords per iteration (half the loop control; adjacent reads pair into ds_read2)
     const int F1 = F < cross ? F : cross;   // dwords before the row's pad dword
-    for (; m + 1 < F1; m += 2) h = sdbm_dword_fast(sdbm_dword_fast(h, p[m]), p[m + 1]);
-    if (m < F1) h = sdbm_dword_fast(h, p[m++]);
-    for (; m + 1 < F; m += 2) h = sdbm_dword_fast(sdbm_dword_fast(h, p[m + 1]), p[m + 2]);
-    if (m < F) h = sdbm_dword_fast(h, p[1 + m++]);
+    for (; m + 3 < F1; m += 4)
+        h = sdbm_dword_fast(sdbm_dword_fast(sdbm_dword_fast(sdbm_dword_fast(h, p[m]), p[m + 1]), p[m + 2]), p[m + 3]);
+    for (; m < F1; ++m) h = sdbm_dword_fast(h, p[m]);
+    for (; m + 3 < F; m += 4)
+        h = sdbm_dword_fast(sdbm_dword_fast(sdbm_dword_fast(sdbm_dword_fast(h, p[m + 1]), p[m + 2]), p[m + 3]), p[m + 4]);
+    for (; m < F; ++m) h = sdbm_dword_fast(h, p[m + 1]);
     if (rem) h = sdbm_dword_fast(h, p[m + (m >= cross ? 1 : 0)] & ((1u << (8 * rem)) - 1u)) * sm.kp_inv[4 - rem];
     return h;
 }
