@@ -44,8 +44,9 @@ CONFIGS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2048)
-    ap.add_argument("--warmup", type=int, default=64)
+    ap.add_argument("--steps", type=int, default=4096)
+    ap.add_argument("--warmup", type=int, default=2048,
+                    help="untimed steps first (about 12 ms at C2: the clocks settle)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batches", type=int, default=64, help="distinct batches in the rotating set")
     ap.add_argument("--per-launch", type=int, default=16,

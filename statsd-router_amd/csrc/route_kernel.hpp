@@ -1242,9 +1242,9 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
             const int c_pre = sm.c_pre;
             const int nwin = min(kWin, (int)tile_count - wbase);
             // lanes per line from the mean line length: 64-byte hash segments per lane
-            const int mean = kTileB / max((int)tile_count, 1);
+            // (G * 64 < kTileB / tile_count, without the division)
             int G = 1;
-            while (G < 32 && G * 64 < mean) G <<= 1;
+            while (G < 32 && (G * 64 + 1) * (int)tile_count <= kTileB) G <<= 1;
             const int nG = BLOCK / G, gi = tid & (G - 1);
             // wave-uniform rounds (the base resolution below needs every lane of the wave)
             for (int jr = 0; jr < nwin; jr += nG) {
@@ -1325,6 +1325,9 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
         if (p.nb > 1000000u) p.ctl->pad1 = pad[(tid + 1) & 1023];
     }
     if (blockIdx.x < p.nb) {   // scanner of batch blockIdx.x (wave 0; no barriers on this path)
+        // the scanner is the latency-critical link of every tile's record base: its few
+        // instructions go ahead of the co-resident tiles' VALU work
+        __builtin_amdgcn_s_setprio(3);
         const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (ABL & ABL_OLD_SCANNER) {
             if (wave == 0) scan_batch<BLOCK>(p, p.b[blockIdx.x], ep0, lane);
