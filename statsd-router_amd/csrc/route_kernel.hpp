@@ -77,6 +77,8 @@ enum : unsigned {
                              // the pipelined scanner publishes ahead of need)
     ABL_AGENT_GRANULES = 262144u,  // every count / base granule stored sc1 (round-1 v0.5), whatever the XCDs
     ABL_SCAN_SERIAL = 524288u,  // round-1 v0.6 scanner: 256 granules per round trip, one poll in flight
+    ABL_MIXED_LANES = 1048576u,  // per-line lane groups for tiles of mixed line lengths (opt-in: C5 -13 %,
+                                 // but its classification costs C2 / C4 2-5 % in registers)
     ABL_OLD_HASH = 1024u,   // round-1 v0.5 per-segment sdbm (v_alignbyte reads, compiler-extracted bytes)
 };
 
@@ -514,6 +516,9 @@ struct SmemT {
     int32_t lend[kWin + 1];          // per staged line: tile position of its '\n'; slot 0 = previous
     int32_t lcol[kWin + 1];          // per staged line: first ':' in the tile part (kNone if none)
     uint32_t wave_cnt[kWaves];
+    uint32_t ccnt[kWaves][6];        // per wave: lines of the window per lane class
+    uint32_t ctab[6];                // per lane class: (first lane << 16) | first sorted slot
+    uint8_t lorder[kWin];            // the window's lines sorted by lane class, largest first
     uint32_t wave_scan[kWaves][4];   // per wave, inclusive at its last lane: '\n' count, latest '\n' lane, colon key
     uint64_t kp_lo[kPowLo];          // K^i
     uint64_t kp_hi[kPowHi];          // K^(64 i)
@@ -1245,11 +1250,11 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
             // (G * 64 < kTileB / tile_count, without the division)
             int G = 1;
             while (G < 32 && (G * 64 + 1) * (int)tile_count <= kTileB) G <<= 1;
-            const int nG = BLOCK / G, gi = tid & (G - 1);
-            // wave-uniform rounds (the base resolution below needs every lane of the wave)
-            for (int jr = 0; jr < nwin; jr += nG) {
-                const int jj = jr + tid / G;
-                const bool act = jj < nwin;
+            // One line's work: bounds, verdict, sdbm (lane gi of the line's Gl lanes takes the
+            // 64-byte segments gi, gi + Gl, ...), shard, record. Gw: the wave-uniform bound of
+            // the lane groups (groups are aligned to their size, so xor partners below Gl stay
+            // inside the group).
+            auto line = [&](int jj, bool act, int gi, int Gl, int Gw) {
                 const int j = wbase + jj;
                 const int e = act ? sm.lend[jj + 1] : 0;
                 int c = act ? sm.lcol[jj + 1] : kNone;
@@ -1262,14 +1267,17 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 if (act && len_ok && fmt_ok && !(ABL & ABL_NO_HASH)) {
                     // sdbm of [s, c) = sum over 64-byte segments k of Horner(seg_k) * K^(c - end_k)
                     const int n = c - s, nseg = (n + 63) >> 6;
-                    for (int k = gi; k < nseg; k += G) {
+                    for (int k = gi; k < nseg; k += Gl) {
                         const int a = s + 64 * k, nn = min(64, n - 64 * k);
                         uint64_t hs = (ABL & ABL_OLD_HASH) ? sdbm_lds(sm, a + kHalo, nn) : sdbm_img(sm, a + kHalo, nn);
                         if (k + 1 < nseg) hs *= kpow_n(sm, c - a - nn);   // the last segment ends at c
                         h += hs;
                     }
                 }
-                for (int d = G >> 1; d >= 1; d >>= 1) h += shfl_xor64(h, d);
+                for (int d = Gw >> 1; d >= 1; d >>= 1) {
+                    const uint64_t v = shfl_xor64(h, d);
+                    if (d < Gl) h += v;
+                }
                 if (act && gi == 0) {
                     uint32_t route;
                     if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
@@ -1279,26 +1287,128 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     r.offset = (uint32_t)(T0 + s);
                     r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
                     r.route = (uint16_t)route;
-                    {
-                        if (!have_base) {   // needed only now, after the hash: normally long published
-                            stamp<ABL>(p, tid, g, 3);
-                            base = granule_ok(st_early, epoch & 0x3FFFFFFFu, kFlagBase)
-                                       ? (uint32_t)st_early
-                                       : wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
-                            stamp<ABL>(p, tid, g, 7);
-                            have_base = true;
+                    if (!have_base) {   // needed only now, after the hash: normally long published
+                        stamp<ABL>(p, tid, g, 3);
+                        base = granule_ok(st_early, epoch & 0x3FFFFFFFu, kFlagBase)
+                                   ? (uint32_t)st_early
+                                   : wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
+                        stamp<ABL>(p, tid, g, 7);
+                        have_base = true;
+                    }
+                    const uint32_t rec = base + (uint32_t)j;
+                    if (rec < bd.max_records) {
+                        if (route == kRoutePending) {
+                            const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
+                            if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
                         }
-                        const uint32_t rec = base + (uint32_t)j;
-                        if (rec < bd.max_records) {
-                            if (route == kRoutePending) {
-                                const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
-                                if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
-                            }
-                            bd.recs[rec] = r;
-                            if (bd.hashes) bd.hashes[rec] = h;
-                        }
+                        bd.recs[rec] = r;
+                        if (bd.hashes) bd.hashes[rec] = h;
                     }
                 }
+            };
+            // Lane classes: thread tid describes line tid of the window; class k = log2 of the
+            // lanes its hash wants (2^k >= its 64-byte segments, at most 32).
+            int ncl = 0;
+            uint32_t TL = 0, Gmax = 1;   // lanes all lines want; the largest class
+            // only tiles of long lines on average (G > 1) can gain; C2-like tiles skip this
+            const bool classify = (ABL & ABL_MIXED_LANES) && G > 1;
+            if (classify) {
+                if (tid < nwin) {
+                    const int jj = tid, j = wbase + jj;
+                    const int e = sm.lend[jj + 1];
+                    int c = sm.lcol[jj + 1];
+                    if (j == 0 && c_pre != kNone) c = c_pre;
+                    const int s = (j == 0) ? s_pre : sm.lend[jj] + 1;
+                    const int len = e - s + 1;
+                    if (len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH && c != kNone && c < e) {
+                        const int nseg = (c - s + 63) >> 6;
+                        ncl = nseg <= 1 ? 0 : min(5, 32 - __builtin_clz((unsigned)(nseg - 1)));
+                    }
+                }
+                const uint32_t want = tid < nwin ? 1u << ncl : 0u;
+                const uint32_t wsum = wave_add32(want);
+                const uint32_t wmax = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max32(want), 63);
+                if (lane == 0) {
+                    sm.ccnt[wave][0] = wsum;
+                    sm.ccnt[wave][1] = wmax;
+                }
+                wg_barrier();
+                uint32_t cls_or = 0;
+#pragma unroll
+                for (int w = 0; w < kWaves; ++w) {
+                    TL += sm.ccnt[w][0];
+                    cls_or = max(cls_or, sm.ccnt[w][1]);
+                }
+                TL = __builtin_amdgcn_readfirstlane(TL);
+                Gmax = max(1u, (uint32_t)__builtin_amdgcn_readfirstlane(cls_or));
+            }
+            // Rounds either way: the tile-wide G (every line G lanes; a longer line's lanes walk
+            // several segments) or one lane group per line sized to the line (groups packed in
+            // descending size). The latter wins on mixed lengths (C5).
+            const int cost_tile = ((nwin * G + BLOCK - 1) / BLOCK) * (((int)Gmax + G - 1) / G);
+            const int cost_mixed = ((int)TL + BLOCK - 1) / BLOCK + 1;
+            const bool mixed = classify && cost_mixed <= cost_tile;
+            if (mixed) {
+                // counting sort of the window's lines by class, largest first, into sm.lorder;
+                // sm.ctab[k] = (first lane of class k << 16) | (first sorted slot of class k)
+                uint32_t rank = 0;
+                wg_barrier();   // every wave has read the totals before ccnt is reused
+#pragma unroll
+                for (int k = 0; k < 6; ++k) {
+                    const uint64_t m = __ballot(tid < nwin && ncl == k);
+                    if (lane == 0) sm.ccnt[wave][k] = (uint32_t)__popcll(m);
+                    if (ncl == k) rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                }
+                wg_barrier();
+                if (tid == 0) {
+                    uint32_t lo = 0, first = 0;
+                    for (int k = 5; k >= 0; --k) {
+                        uint32_t n = 0;
+                        for (int w = 0; w < kWaves; ++w) n += sm.ccnt[w][k];
+                        sm.ctab[k] = (lo << 16) | first;
+                        lo += n << k;
+                        first += n;
+                    }
+                }
+                wg_barrier();
+                if (tid < nwin) {
+                    uint32_t pos = (sm.ctab[ncl] & 0xFFFFu) + rank;
+                    for (int w = 0; w < wave; ++w) pos += sm.ccnt[w][ncl];
+                    sm.lorder[pos] = (uint8_t)tid;
+                }
+                wg_barrier();
+            }
+            // wave-uniform rounds over the lanes the lines want (the base resolution needs every
+            // lane of the wave): tile-wide G, or the sorted per-line groups
+            const int lanes_total = mixed ? (int)TL : nwin * G;
+            const int Gw = mixed ? (int)Gmax : G;
+            for (int r0 = 0; r0 < lanes_total; r0 += BLOCK) {
+                const uint32_t x = (uint32_t)(r0 + tid);
+                int jj, gi, Gl;
+                bool act;
+                if (!mixed) {
+                    jj = (int)(x >> __builtin_ctz((unsigned)G));
+                    gi = (int)(x & (uint32_t)(G - 1));
+                    Gl = G;
+                    act = jj < nwin;
+                } else {
+                    // the class whose lane range [lo_k, lo_(k-1)) holds x (class 5 starts at lane 0)
+                    int k = -1;
+#pragma unroll
+                    for (int kk = 5; kk >= 0; --kk) {
+                        const uint32_t lo = sm.ctab[kk] >> 16;
+                        const uint32_t hi = kk ? (sm.ctab[kk - 1] >> 16) : TL;
+                        if (k < 0 && x >= lo && x < hi) k = kk;
+                    }
+                    act = k >= 0;
+                    const int kc = act ? k : 0;
+                    const uint32_t t = sm.ctab[kc];
+                    const uint32_t off = act ? x - (t >> 16) : 0u;
+                    jj = act ? (int)sm.lorder[(t & 0xFFFFu) + (off >> kc)] : 0;
+                    gi = (int)(off & ((1u << kc) - 1u));
+                    Gl = 1 << kc;
+                }
+                line(jj, act, gi, Gl, Gw);
             }
         }
 
