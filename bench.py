@@ -49,7 +49,7 @@ def parse():
                     help="untimed steps first (about 12 ms at C2: the clocks settle)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batches", type=int, default=64, help="distinct batches in the rotating set")
-    ap.add_argument("--per-launch", type=int, default=16,
+    ap.add_argument("--per-launch", type=int, default=32,
                     help="batches routed per kernel launch (sr_route_device_many; 1 = sr_route_device)")
     ap.add_argument("--dead", type=float, default=0.0, help="fraction of dead downstreams")
     ap.add_argument("--regroup", default="auto", choices=["auto", "on", "off"],
