@@ -585,7 +585,7 @@ __device__ __forceinline__ uint64_t sdbm_img(const S &sm, int a, int n) {
     if (F == 0) return sdbm_dword_fast(0, first & ((1u << (8 * rem)) - 1u)) * sm.kp_inv[4 - rem];
     uint64_t h = sdbm_dword_fast(0, first);
     int m = 1;
-    // two dwords per iteration (half the loop control; adjacent reads pair into ds_read2)
+    // four dwords per iteration (a quarter of the loop control; adjacent reads pair into ds_read2)
     const int F1 = F < cross ? F : cross;   // dwords before the row's pad dword
     for (; m + 3 < F1; m += 4)
         h = sdbm_dword_fast(sdbm_dword_fast(sdbm_dword_fast(sdbm_dword_fast(h, p[m]), p[m + 1]), p[m + 2]), p[m + 3]);
