@@ -322,3 +322,32 @@ def test_device_many_records_only(pkg, oracle):
             recs = d_out[i].cpu().numpy().view(pkg.RECORD_DTYPE)[:k]
             exp, _, en = oracle.route(p, 16)
             assert k == en and np.array_equal(recs, exp), f"batch {i}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nb", [2, 5, 7, 8, 32])
+def test_device_many_class_tables(pkg, oracle, nb):
+    """Batch lookup table (cls_tab) shapes: 2-7 batches share one class (no XCD-local dealing),
+    8 and 32 are dealt to the 8 XCD classes; sizes differ a lot so classes are unbalanced and
+    padding blocks appear."""
+    import torch
+
+    rng = random.Random(1000 + nb)
+    parts = [pkg.gen_stream(rng.choice([900, 40_000, 300_000, 2_000_000]), rng.choice([[64], [256], [64, 1024]]),
+                            seed=1100 + nb * 40 + i, p_invalid=0.05).data for i in range(nb)]
+    with pkg.Router(9, 2 << 20) as r:
+        r.set_stream(torch.cuda.current_stream().cuda_stream)
+        d_in = [torch.from_numpy(p.copy()).to("cuda") for p in parts]
+        d_out = [torch.empty(int(p.size) * 8, dtype=torch.uint8, device="cuda") for p in parts]
+        d_n = torch.full((nb,), -1, dtype=torch.int64, device="cuda")
+        descs = [(d_in[i].data_ptr(), int(p.size), d_out[i].data_ptr(), int(p.size), None, d_n.data_ptr() + 8 * i)
+                 for i, p in enumerate(parts)]
+        for _ in range(2):
+            r.route_device_many(descs)
+        torch.cuda.synchronize()
+        counts = d_n.cpu().numpy()
+        for i, p in enumerate(parts):
+            k = int(counts[i])
+            recs = d_out[i].cpu().numpy().view(pkg.RECORD_DTYPE)[:k]
+            exp, _, en = oracle.route(p, 9)
+            assert k == en and np.array_equal(recs, exp), f"{nb} batches: batch {i}"
