@@ -79,6 +79,7 @@ enum : unsigned {
     ABL_SCAN_SERIAL = 524288u,  // round-1 v0.6 scanner: 256 granules per round trip, one poll in flight
     ABL_MIXED_LANES = 1048576u,  // per-line lane groups for tiles of mixed line lengths (opt-in: C5 -13 %,
                                  // but its classification costs C2 / C4 2-5 % in registers)
+    ABL_NO_MID_BASE = 2097152u,  // no base read part-way through the hash (round-1 v0.8)
     ABL_OLD_HASH = 1024u,   // round-1 v0.5 per-segment sdbm (v_alignbyte reads, compiler-extracted bytes)
 };
 
@@ -575,8 +576,11 @@ __device__ __forceinline__ uint64_t sdbm_lds(const S &sm, int a, int n) {
 // bytes of the first dword before a are zeroed (leading zeros leave a Horner value unchanged), the
 // last partial dword is zero-padded and the padding undone by K^-z. Dword m of the run is p[m]
 // before the row's pad dword and p[m + 1] after it.
+// slot != nullptr: also read that granule into st part-way through (after the dwords before
+// the row's pad): the tile's record base, requested about a round trip before it is needed.
 template <class S>
-__device__ __forceinline__ uint64_t sdbm_img(const S &sm, int a, int n) {
+__device__ __forceinline__ uint64_t sdbm_img(const S &sm, int a, int n, const uint64_t *slot = nullptr,
+                                             uint64_t *st = nullptr) {
     const int lead = a & 3, L = lead + n;
     const int F = L >> 2, rem = L & 3;
     const int dw = a >> 2, s16 = dw & 15, cross = 16 - s16;
@@ -590,6 +594,7 @@ __device__ __forceinline__ uint64_t sdbm_img(const S &sm, int a, int n) {
     for (; m + 3 < F1; m += 4)
         h = sdbm_dword_fast(sdbm_dword_fast(sdbm_dword_fast(sdbm_dword_fast(h, p[m]), p[m + 1]), p[m + 2]), p[m + 3]);
     for (; m < F1; ++m) h = sdbm_dword_fast(h, p[m]);
+    if (slot) *st = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (; m + 3 < F; m += 4)
         h = sdbm_dword_fast(sdbm_dword_fast(sdbm_dword_fast(sdbm_dword_fast(h, p[m + 1]), p[m + 2]), p[m + 3]), p[m + 4]);
     for (; m < F; ++m) h = sdbm_dword_fast(h, p[m + 1]);
@@ -1269,7 +1274,9 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     const int n = c - s, nseg = (n + 63) >> 6;
                     for (int k = gi; k < nseg; k += Gl) {
                         const int a = s + 64 * k, nn = min(64, n - 64 * k);
-                        uint64_t hs = (ABL & ABL_OLD_HASH) ? sdbm_lds(sm, a + kHalo, nn) : sdbm_img(sm, a + kHalo, nn);
+                        const bool mid = !(ABL & (ABL_NO_MID_BASE | ABL_EARLY_BASE)) && !have_base && k == gi;
+                        uint64_t hs = (ABL & ABL_OLD_HASH) ? sdbm_lds(sm, a + kHalo, nn)
+                                                           : sdbm_img(sm, a + kHalo, nn, mid ? base_slot : nullptr, &st_early);
                         if (k + 1 < nseg) hs *= kpow_n(sm, c - a - nn);   // the last segment ends at c
                         h += hs;
                     }

@@ -53,6 +53,7 @@ static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream
         if (!strcmp(e, "agent_granules")) return 11;
         if (!strcmp(e, "scan_serial")) return 12;
         if (!strcmp(e, "mixed_lanes")) return 13;
+        if (!strcmp(e, "no_mid_base")) return 14;
         // upper bounds, not routing (records wrong or missing; line counts still exact)
         if (!strcmp(e, "fake_base")) return 7;
         if (!strcmp(e, "no_hash")) return 8;
@@ -71,6 +72,7 @@ static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream
     case 11: return launch_route<kBlock, ABL_AGENT_GRANULES>(ds, p, stream);
     case 12: return launch_route<kBlock, ABL_SCAN_SERIAL>(ds, p, stream);
     case 13: return launch_route<kBlock, ABL_MIXED_LANES>(ds, p, stream);
+    case 14: return launch_route<kBlock, ABL_NO_MID_BASE>(ds, p, stream);
     case 7: return launch_route<kBlock, ABL_FAKE_BASE>(ds, p, stream);
     case 8: return launch_route<kBlock, ABL_NO_HASH>(ds, p, stream);
     case 9: return launch_route<kBlock, ABL_NO_LINES>(ds, p, stream);
