@@ -283,12 +283,15 @@ def regroup_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, B, max_lin
     d_rec = torch.empty(max_lines, dtype=torch.int64, device=dev)
     d_n = torch.zeros(1, dtype=torch.int64, device=dev)
     base = d_in.data_ptr()
+    rank = dist.get_rank()
 
     def step(i):
         b = i % B
         router.route_device(base + b * batch_bytes, sizes[b], d_rec.data_ptr(), max_lines, None, d_n.data_ptr())
         rb, rr, rc = reg(base + b * batch_bytes, sizes[b], d_rec.data_ptr(), d_n.data_ptr(), max_lines)
-        return int(rr.numel()), int(rb.numel()), int(reg.counts[:, 1].sum().item() - reg.counts[dist.get_rank(), 1].item())
+        # bytes this rank sent to the other ranks, from the host copy the exchange already made
+        sent = sum(c[1] for c in reg.last_sent) - reg.last_sent[rank][1]
+        return int(rr.numel()), int(rb.numel()), sent
 
     with torch.cuda.stream(stream):
         for i in range(2):
