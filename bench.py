@@ -279,32 +279,39 @@ def regroup_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, B, max_lin
     rg_mod = importlib.import_module("statsd-router_amd.regroup")
     if world == 1 and not dist.is_initialized():
         dist.init_process_group("nccl", store=dist.TCPStore("127.0.0.1", 0, 1, True), rank=0, world_size=1)
-    reg = rg_mod.Regrouper(pkg, router, batch_bytes, max_lines)
+    reg = rg_mod.Regrouper(pkg, router, batch_bytes, max_lines, slots=2)
     d_rec = torch.empty(max_lines, dtype=torch.int64, device=dev)
     d_n = torch.zeros(1, dtype=torch.int64, device=dev)
     base = d_in.data_ptr()
     rank = dist.get_rank()
 
-    def step(i):
+    def start(i):
         b = i % B
         router.route_device(base + b * batch_bytes, sizes[b], d_rec.data_ptr(), max_lines, None, d_n.data_ptr())
-        rb, rr, rc = reg(base + b * batch_bytes, sizes[b], d_rec.data_ptr(), d_n.data_ptr(), max_lines)
+        reg.start(i % 2, base + b * batch_bytes, sizes[b], d_rec.data_ptr(), d_n.data_ptr(), max_lines)
+
+    def finish(i):
+        rb, rr, _ = reg.finish(i % 2)
         # bytes this rank sent to the other ranks, from the host copy the exchange already made
         sent = sum(c[1] for c in reg.last_sent) - reg.last_sent[rank][1]
         return int(rr.numel()), int(rb.numel()), sent
 
+    def run(n):
+        # two slots: batch i+1 is routed and packed while the host waits for batch i's split sizes
+        acc = [0, 0, 0]
+        start(0)
+        for i in range(n):
+            if i + 1 < n:
+                start(i + 1)
+            acc = [a + x for a, x in zip(acc, finish(i))]
+        return acc
+
     with torch.cuda.stream(stream):
-        for i in range(2):
-            step(i)
+        run(2)
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        recv_lines = recv_bytes = sent_off = 0
-        for i in range(steps):
-            a, b_, c = step(i)
-            recv_lines += a
-            recv_bytes += b_
-            sent_off += c
+        recv_lines, recv_bytes, sent_off = run(steps)
         torch.cuda.synchronize()
         dist.barrier()
         wall = time.perf_counter() - t0
@@ -319,7 +326,8 @@ def regroup_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, B, max_lin
             "lines_regrouped": int(tot[1]), "bytes_regrouped": int(tot[2]),
             "bytes_sent_to_other_gpus_per_s": round(float(tot[3]) / w / 1e9, 3),
             "note": (f"route + sr_pack_by_owner + all-to-all (split sizes, packed lines, records) per 16 MiB batch "
-                     f"over {world} GPU(s); owner = shard % {world}; host round trip for the split sizes")}
+                     f"over {world} GPU(s); owner = shard % {world}; host round trip for the split sizes, "
+                     f"two slots: batch i+1 routed and packed while batch i's sizes come back")}
 
 
 def e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M, groups=24):

@@ -242,7 +242,11 @@ class Router:
         _check(self._lib.sr_set_alive(self._h, w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))), "sr_set_alive")
 
     def set_stream(self, stream_handle: int | None) -> None:
+        """Launch on this HIP stream from now on. 0/None = the context's own non-blocking stream
+        (sr_set_stream's NULL), which is NOT the HIP null stream: work on torch's default stream
+        is not ordered with it."""
         _check(self._lib.sr_set_stream(self._h, ctypes.c_void_p(stream_handle or 0)), "sr_set_stream")
+        self.stream_handle = int(stream_handle or 0)
 
     def route(self, data: bytes | np.ndarray, max_records: int | None = None, want_hashes: bool = False):
         """sr_route_batch on host memory. Returns (records[n] structured array, hashes or None, n)."""

@@ -17,16 +17,18 @@ import torch
 import torch.distributed as dist
 
 
-def _exchange(packed_bytes, packed_recs, owner_counts, group):
-    """exchange_packed, also returning the host copies of the split sizes ([G, 2] lists sent and
-    received). One host round trip per exchange: the sent and received sizes come back in one copy,
-    and the offset rebase runs on the device from the received sizes (no host-built tensors)."""
+def _exchange_sizes(owner_counts, both, group):
+    """First half of an exchange: all-to-all of the split sizes into both[1] (both[0] = ours).
+    both: int64 [2, G, 2] on the packing device."""
     G = dist.get_world_size(group)
-    dev = packed_bytes.device
-    both = torch.empty((2, G, 2), dtype=torch.int64, device=dev)
     both[0].copy_(owner_counts.reshape(G, 2))
     dist.all_to_all_single(both[1], both[0], group=group)
-    send, recv = both.cpu().tolist()
+
+
+def _exchange_data(packed_bytes, packed_recs, recv_counts, send, recv, group):
+    """Second half: all-to-all of the packed lines and records with the host copies of the split
+    sizes, then the offset rebase on the device from the received sizes (no host-built tensors)."""
+    dev = packed_bytes.device
     in_l, in_b = [c[0] for c in send], [c[1] for c in send]
     out_l, out_b = [c[0] for c in recv], [c[1] for c in recv]
     n_l, n_b = sum(out_l), sum(out_b)
@@ -34,14 +36,24 @@ def _exchange(packed_bytes, packed_recs, owner_counts, group):
     dist.all_to_all_single(recv_bytes, packed_bytes[: sum(in_b)], out_b, in_b, group=group)
     recv_recs = torch.empty(n_l, dtype=torch.int64, device=dev)
     dist.all_to_all_single(recv_recs, packed_recs[: sum(in_l)], out_l, in_l, group=group)
-    recv_counts = both[1]
     if n_l:
         # record offset = low 32 bits (little-endian {u32 offset, u16 length, u16 route}); every
         # rebased offset stays below 2^32, so a 64-bit add never carries into length/route.
         # base[s] = bytes received from ranks before s (exclusive scan, on the device)
         base = torch.cumsum(recv_counts[:, 1], 0) - recv_counts[:, 1]
         recv_recs += torch.repeat_interleave(base, recv_counts[:, 0], output_size=n_l)
-    return recv_bytes, recv_recs, recv_counts, send, recv
+    return recv_bytes, recv_recs
+
+
+def _exchange(packed_bytes, packed_recs, owner_counts, group):
+    """exchange_packed, also returning the host copies of the split sizes ([G, 2] lists sent and
+    received). One host round trip per exchange: the sent and received sizes come back in one copy."""
+    G = dist.get_world_size(group)
+    both = torch.empty((2, G, 2), dtype=torch.int64, device=packed_bytes.device)
+    _exchange_sizes(owner_counts, both, group)
+    send, recv = both.cpu().tolist()
+    rb, rr = _exchange_data(packed_bytes, packed_recs, both[1], send, recv, group)
+    return rb, rr, both[1], send, recv
 
 
 def exchange_packed(packed_bytes: torch.Tensor, packed_recs: torch.Tensor, owner_counts: torch.Tensor,
@@ -56,9 +68,16 @@ def exchange_packed(packed_bytes: torch.Tensor, packed_recs: torch.Tensor, owner
 
 
 class Regrouper:
-    """Pack (HIP) + exchange for one Router context; buffers sized for one batch."""
+    """Pack (HIP) + exchange for one Router context; buffers sized for one batch per slot.
 
-    def __init__(self, pkg, router, max_batch_bytes: int, max_records: int, group=None):
+    Synchronous use: `reg(...)` packs and exchanges one batch. Pipelined use (two slots):
+    `start(slot, ...)` packs a batch and launches the all-to-all of its split sizes plus their
+    copy to pinned host memory; `finish(slot)` waits for that copy and exchanges the lines. Calling
+    start(i+1) before finish(i) lets batch i+1's route and pack run on the GPU while the host waits
+    for batch i's sizes. All calls go on the router's stream (= torch's current one), so a slot's
+    buffers are rewritten only after its exchange in stream order."""
+
+    def __init__(self, pkg, router, max_batch_bytes: int, max_records: int, group=None, slots: int = 1):
         self.pkg, self.router, self.group = pkg, router, group
         self.G = dist.get_world_size(group)
         if not 1 <= self.G <= pkg.SR_MAX_OWNERS:
@@ -66,25 +85,61 @@ class Regrouper:
         dev = torch.device("cuda", router.device)
         self.cap = pkg.pack_capacity(max_batch_bytes)
         self.max_records = max_records
-        self.out_bytes = torch.empty(self.cap, dtype=torch.uint8, device=dev)
-        self.out_recs = torch.empty(max(max_records, 1), dtype=torch.int64, device=dev)
-        self.counts = torch.zeros((self.G, 2), dtype=torch.int64, device=dev)
+        self.slots = [self._slot(dev) for _ in range(max(slots, 1))]
         # host copies of the last exchange's split sizes ([G][lines, bytes] sent and received)
         self.last_sent: list = []
         self.last_received: list = []
 
-    def pack(self, d_bytes: int, nbytes: int, d_recs: int, d_n_records: int, max_records: int) -> None:
+    def _slot(self, dev):
+        return {"bytes": torch.empty(self.cap, dtype=torch.uint8, device=dev),
+                "recs": torch.empty(max(self.max_records, 1), dtype=torch.int64, device=dev),
+                "counts": torch.zeros((self.G, 2), dtype=torch.int64, device=dev),
+                "both": torch.empty((2, self.G, 2), dtype=torch.int64, device=dev),
+                "h_both": torch.empty((2, self.G, 2), dtype=torch.int64, pin_memory=True),
+                "ev": torch.cuda.Event()}
+
+    @property
+    def counts(self):
+        return self.slots[0]["counts"]
+
+    def _check_stream(self):
+        # the collectives are ordered after torch's current stream; the pack must run on it too
+        h = getattr(self.router, "stream_handle", 0)
+        if h == 0 or h != torch.cuda.current_stream().cuda_stream:
+            raise RuntimeError("Regrouper: router.set_stream(s.cuda_stream) with s = torch's current stream "
+                               "(a non-default stream) is required")
+
+    def pack(self, d_bytes: int, nbytes: int, d_recs: int, d_n_records: int, max_records: int,
+             slot: int = 0) -> None:
+        self._check_stream()
         if max_records > self.max_records:
             raise ValueError("max_records exceeds the regrouper's record buffer")
+        sl = self.slots[slot]
         self.router.pack_by_owner(d_bytes, nbytes, d_recs, d_n_records, max_records, self.G,
-                                  self.out_bytes.data_ptr(), self.cap, self.out_recs.data_ptr(),
-                                  self.counts.data_ptr())
+                                  sl["bytes"].data_ptr(), self.cap, sl["recs"].data_ptr(),
+                                  sl["counts"].data_ptr())
 
-    def exchange(self):
+    def exchange(self, slot: int = 0):
         """Pack output -> all-to-all (call after pack, on the router's stream = torch's current one)."""
-        rb, rr, rc, self.last_sent, self.last_received = _exchange(self.out_bytes, self.out_recs, self.counts,
+        sl = self.slots[slot]
+        rb, rr, rc, self.last_sent, self.last_received = _exchange(sl["bytes"], sl["recs"], sl["counts"],
                                                                    self.group)
         return rb, rr, rc
+
+    def start(self, slot: int, d_bytes: int, nbytes: int, d_recs: int, d_n_records: int, max_records: int):
+        sl = self.slots[slot]
+        self.pack(d_bytes, nbytes, d_recs, d_n_records, max_records, slot)
+        _exchange_sizes(sl["counts"], sl["both"], self.group)
+        sl["h_both"].copy_(sl["both"], non_blocking=True)
+        sl["ev"].record()
+
+    def finish(self, slot: int):
+        sl = self.slots[slot]
+        sl["ev"].synchronize()
+        self.last_sent, self.last_received = sl["h_both"].tolist()
+        rb, rr = _exchange_data(sl["bytes"], sl["recs"], sl["both"][1], self.last_sent, self.last_received,
+                                self.group)
+        return rb, rr, sl["both"][1].clone()
 
     def __call__(self, d_bytes: int, nbytes: int, d_recs: int, d_n_records: int, max_records: int):
         self.pack(d_bytes, nbytes, d_recs, d_n_records, max_records)

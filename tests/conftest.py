@@ -54,3 +54,20 @@ def load_case(name):
 def load_digests():
     with open(os.path.join(GOLDEN, "digests.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture
+def torch_stream():
+    """A fresh torch stream made current for the test: the router is set to it, so torch's copies
+    and fills, the HIP kernels and the collectives are ordered on one stream. (Router.set_stream(0)
+    means the context's own non-blocking stream, not torch's default stream.)"""
+    import torch
+
+    prev = torch.cuda.current_stream()
+    s = torch.cuda.Stream()
+    torch.cuda.set_stream(s)
+    try:
+        yield s
+    finally:
+        torch.cuda.synchronize()
+        torch.cuda.set_stream(prev)

@@ -189,7 +189,7 @@ def test_empty_and_unterminated_batches(pkg, router_factory):
     assert ei.value.errno == errno.EINVAL
 
 
-def test_device_resident_path(pkg, oracle):
+def test_device_resident_path(pkg, oracle, torch_stream):
     import torch
 
     s = pkg.gen_stream(16 << 20, [64], seed=0x5EED0002)
@@ -198,8 +198,7 @@ def test_device_resident_path(pkg, oracle):
         d_out = torch.empty(s.n_lines * 8, dtype=torch.uint8, device="cuda")
         d_h = torch.empty(s.n_lines, dtype=torch.int64, device="cuda")
         d_n = torch.zeros(1, dtype=torch.int64, device="cuda")
-        stream = torch.cuda.current_stream()
-        r.set_stream(stream.cuda_stream)
+        r.set_stream(torch_stream.cuda_stream)
         for _ in range(3):
             r.route_device(d_in.data_ptr(), s.data.size, d_out.data_ptr(), s.n_lines, d_h.data_ptr(), d_n.data_ptr())
         torch.cuda.synchronize()
@@ -209,7 +208,7 @@ def test_device_resident_path(pkg, oracle):
 
 
 @pytest.mark.parametrize("dead", [0, 1, 20])
-def test_device_many_batches_one_launch(pkg, oracle, dead):
+def test_device_many_batches_one_launch(pkg, oracle, dead, torch_stream):
     """sr_route_device_many: batches of different shapes (incl. empty and tiny ones) routed in one
     launch, each exactly as the oracle routes it alone; 20 dead of 40 takes the wide probe path
     (one launch per batch)."""
@@ -227,8 +226,7 @@ def test_device_many_batches_one_launch(pkg, oracle, dead):
     ] + [pkg.gen_stream(70_000 + 9_999 * i, [64, 256, 1024], seed=20 + i).data for i in range(14)]
     with pkg.Router(n, 4 << 20) as r:
         r.set_alive(alive)
-        stream = torch.cuda.current_stream()
-        r.set_stream(stream.cuda_stream)
+        r.set_stream(torch_stream.cuda_stream)
         d_in, d_out, d_h, descs = [], [], [], []
         d_n = torch.full((len(parts),), -1, dtype=torch.int64, device="cuda")
         for i, p in enumerate(parts):
@@ -249,14 +247,14 @@ def test_device_many_batches_one_launch(pkg, oracle, dead):
             _assert_same((recs, hs, k), oracle.route(p, n, alive), f"batch {i}")
 
 
-def test_device_many_splits_past_launch_limit(pkg, oracle):
+def test_device_many_splits_past_launch_limit(pkg, oracle, torch_stream):
     """More batches than one launch takes (SR_MAX_BATCHES_PER_LAUNCH): split into launches."""
     import torch
 
     n = pkg.SR_MAX_BATCHES_PER_LAUNCH + 9
     parts = [pkg.gen_stream(20_000 + 3_001 * i, [64, 256], seed=400 + i, p_invalid=0.05).data for i in range(n)]
     with pkg.Router(7, 1 << 20) as r:
-        r.set_stream(torch.cuda.current_stream().cuda_stream)
+        r.set_stream(torch_stream.cuda_stream)
         d_in = [torch.from_numpy(p.copy()).to("cuda") for p in parts]
         d_out = [torch.empty(int(p.size) * 8, dtype=torch.uint8, device="cuda") for p in parts]
         d_n = torch.full((n,), -1, dtype=torch.int64, device="cuda")
@@ -299,7 +297,7 @@ def test_hostile_stream_records_only(pkg, oracle, router_factory, seed):
         assert np.array_equal(recs, cr), f"seed {seed}"
 
 
-def test_device_many_records_only(pkg, oracle):
+def test_device_many_records_only(pkg, oracle, torch_stream):
     """16 batches of 4 MiB in one launch (two batches per XCD class), records only, and short-line
     tiles with several windows."""
     import torch
@@ -307,7 +305,7 @@ def test_device_many_records_only(pkg, oracle):
     parts = [pkg.gen_stream(4 << 20, [[64], [256], [64, 256, 1024], [16, 24]][i % 4], seed=800 + i,
                             p_invalid=0.05 * (i % 3)).data for i in range(16)]
     with pkg.Router(16, 4 << 20) as r:
-        r.set_stream(torch.cuda.current_stream().cuda_stream)
+        r.set_stream(torch_stream.cuda_stream)
         d_in = [torch.from_numpy(p.copy()).to("cuda") for p in parts]
         d_out = [torch.empty(int(p.size) * 8, dtype=torch.uint8, device="cuda") for p in parts]
         d_n = torch.full((16,), -1, dtype=torch.int64, device="cuda")
@@ -326,7 +324,7 @@ def test_device_many_records_only(pkg, oracle):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nb", [2, 5, 7, 8, 32])
-def test_device_many_class_tables(pkg, oracle, nb):
+def test_device_many_class_tables(pkg, oracle, nb, torch_stream):
     """Batch lookup table (cls_tab) shapes: 2-7 batches share one class (no XCD-local dealing),
     8 and 32 are dealt to the 8 XCD classes; sizes differ a lot so classes are unbalanced and
     padding blocks appear."""
@@ -336,7 +334,7 @@ def test_device_many_class_tables(pkg, oracle, nb):
     parts = [pkg.gen_stream(rng.choice([900, 40_000, 300_000, 2_000_000]), rng.choice([[64], [256], [64, 1024]]),
                             seed=1100 + nb * 40 + i, p_invalid=0.05).data for i in range(nb)]
     with pkg.Router(9, 2 << 20) as r:
-        r.set_stream(torch.cuda.current_stream().cuda_stream)
+        r.set_stream(torch_stream.cuda_stream)
         d_in = [torch.from_numpy(p.copy()).to("cuda") for p in parts]
         d_out = [torch.empty(int(p.size) * 8, dtype=torch.uint8, device="cuda") for p in parts]
         d_n = torch.full((nb,), -1, dtype=torch.int64, device="cuda")

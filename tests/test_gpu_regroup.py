@@ -21,14 +21,14 @@ def _route_on_gpu(pkg, router, data, torch):
 
 
 @pytest.mark.parametrize("G,n_shards,dead", [(1, 4, 0), (2, 64, 0), (3, 16, 2), (8, 64, 5), (64, 100, 0), (5, 3, 3)])
-def test_pack_by_owner_matches_oracle(pkg, oracle, G, n_shards, dead):
+def test_pack_by_owner_matches_oracle(pkg, oracle, G, n_shards, dead, torch_stream):
     import torch
 
     alive = [0 if k < dead else 1 for k in range(n_shards)]
     data = pkg.gen_stream(3 << 20, [64, 256, 1024], seed=900 + G, p_invalid=0.1).data
     with pkg.Router(n_shards, 4 << 20) as r:
         r.set_alive(alive)
-        r.set_stream(torch.cuda.current_stream().cuda_stream)
+        r.set_stream(torch_stream.cuda_stream)
         d_in, d_rec, d_n, cap = _route_on_gpu(pkg, r, data, torch)
         out_cap = pkg.pack_capacity(int(data.size))
         d_pb = torch.full((out_cap,), 0xAB, dtype=torch.uint8, device="cuda")
@@ -50,7 +50,7 @@ def test_pack_by_owner_matches_oracle(pkg, oracle, G, n_shards, dead):
         assert (got_b[tot_b:] == 0xAB).all()   # nothing written past the packed total
 
 
-def test_regrouper_one_rank_rccl(pkg, oracle):
+def test_regrouper_one_rank_rccl(pkg, oracle, torch_stream):
     import torch
     import torch.distributed as dist
 
@@ -61,7 +61,7 @@ def test_regrouper_one_rank_rccl(pkg, oracle):
     try:
         data = pkg.gen_stream(2 << 20, [64, 256], seed=31, p_invalid=0.05).data
         with pkg.Router(8, 4 << 20) as r:
-            r.set_stream(torch.cuda.current_stream().cuda_stream)
+            r.set_stream(torch_stream.cuda_stream)
             d_in, d_rec, d_n, cap = _route_on_gpu(pkg, r, data, torch)
             reg = rg.Regrouper(pkg, r, 4 << 20, cap)
             rb, rr, rc = reg(d_in.data_ptr(), int(data.size), d_rec.data_ptr(), d_n.data_ptr(), cap)
@@ -71,5 +71,39 @@ def test_regrouper_one_rank_rccl(pkg, oracle):
             assert np.array_equal(rb.cpu().numpy(), eb)
             assert np.array_equal(rr.cpu().numpy().view(pkg.RECORD_DTYPE), er)
             assert rc.cpu().tolist() == ec.tolist()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_regrouper_two_slots_pipelined(pkg, oracle, torch_stream):
+    """start(i+1) before finish(i): the two slots' buffers stay apart (one-rank RCCL group)."""
+    import torch
+    import torch.distributed as dist
+
+    rg = importlib.import_module("statsd-router_amd.regroup")
+    store = dist.TCPStore("127.0.0.1", 0, 1, True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1)
+    try:
+        streams = [pkg.gen_stream(1 << 20, [64, 256, 1024], seed=41 + k, p_invalid=0.1).data for k in range(4)]
+        with pkg.Router(16, 2 << 20) as r:
+            r.set_stream(torch_stream.cuda_stream)
+            routed = [_route_on_gpu(pkg, r, d, torch) for d in streams]
+            cap = max(x[3] for x in routed)
+            reg = rg.Regrouper(pkg, r, 2 << 20, cap, slots=2)
+            got = []
+            for i in range(len(streams)):
+                d_in, d_rec, d_n, c = routed[i]
+                reg.start(i % 2, d_in.data_ptr(), int(streams[i].size), d_rec.data_ptr(), d_n.data_ptr(), c)
+                if i:
+                    got.append([t.cpu() for t in reg.finish((i - 1) % 2)])
+            got.append([t.cpu() for t in reg.finish((len(streams) - 1) % 2)])
+            torch.cuda.synchronize()
+            for data, (rb, rr, rc) in zip(streams, got):
+                recs, _, n = oracle.route(data, 16)
+                eb, er, ec = oracle.pack_by_owner(data, recs, 1)
+                assert np.array_equal(rb.numpy(), eb)
+                assert np.array_equal(rr.numpy().view(pkg.RECORD_DTYPE), er)
+                assert rc.tolist() == ec.tolist()
     finally:
         dist.destroy_process_group()
