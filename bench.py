@@ -1,31 +1,41 @@
 #!/usr/bin/env python3
 """Device-resident throughput of the statsd-router hot path on MI355X.
 
-One step = one pass of the hot path (frame-free tokenise -> length/':' validate -> sdbm name hash
--> consistent-hash shard pick, one sr_record per line) over one 16 MiB batch of synthetic framed
-datagrams already resident in HBM (BASELINE.json configs[1], "C2": 64-byte valid metrics, 4
-downstream shards). The timed region cycles through a rotating set of distinct batches (default
-64 x 16 MiB = 1 GiB per GPU, well past the 256 MiB Infinity Cache) launched back to back from a
-captured HIP graph.
+The hot path: newline tokenise -> length / ':' validate -> sdbm name hash ->
+consistent-hash shard pick, one sr_record per line (sr-main.c:86-191), over synthetic framed
+datagrams already resident in HBM.
+
+One STEP = one route_kernel launch over SR_MAX_BATCHES_PER_LAUNCH (32) distinct 16 MiB batches
+(512 MiB of framed datagrams at C2 = BASELINE.json configs[1]: 64-byte valid metrics, 4 downstream
+shards). Consecutive steps alternate over a rotating set of 64 distinct batches (1 GiB per GPU,
+4x the 256 MiB Infinity Cache), each launch replayed from its captured HIP graph. The timed
+region is exactly K steps bracketed by barrier + synchronize; warm-up is W steps and at least
+--min-warmup-ms of back-to-back launches (the clocks settle). roofline.achieved is the timed
+region's bytes over the timed region's GPU time (HIP events on the launch stream).
+
+After timing, the timed configuration itself is checked: one more replay of launch 0, then batch
+0's records are SHA-256 compared with tests/golden/digests.json (the compiled reference's output
+for the same seed) and the launch's last batch is compared record for record with the C oracle.
 
   python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c4|c5]
-  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N  (one rank per GPU,
-  each routing its own datagram batches: weak scaling, no data-path collective)
+  --gpus N > 1 without WORLD_SIZE: re-launches itself under torch.distributed.run (N ranks, one per
+  GPU; each rank routes its own batches: weak scaling, no collective on the classify path) plus a
+  classify + regroup leg over RCCL on C5-shaped batches.
 
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import importlib
 import json
 import os
+import platform
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
-import torch
-import torch.distributed as dist
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
@@ -33,37 +43,96 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 
 CONFIGS = {
-    # name: (description, batch bytes, line lengths, p_invalid, shards, seed base)
-    "c2": ("C2: 16 MiB batch of 64-byte valid metrics, 4 downstream shards", 16 << 20, [64], 0.0, 4, 0x5EED0002),
-    "c3": ("C3: 16 MiB batch of 256-byte metrics, 10% invalid lines, 4 shards", 16 << 20, [256], 0.10, 4, 0x5EED0003),
-    "c4": ("C4: 16 MiB batch of 1024-byte metrics, 16 downstream shards", 16 << 20, [1024], 0.0, 16, 0x5EED0004),
-    "c5": ("C5: 16 MiB batch of mixed 64/256/1024-byte metrics, 64 shards", 16 << 20, [64, 256, 1024], 0.0, 64, 0x5EED0005),
+    # name: (description, batch bytes, line lengths, p_invalid, shards, seed base, digest key)
+    "c2": ("C2: 16 MiB batches of 64-byte valid metrics, 4 downstream shards", 16 << 20, [64], 0.0, 4, 0x5EED0002,
+           "c2_64B_n4"),
+    "c3": ("C3: 16 MiB batches of 256-byte metrics, 10% invalid lines, 4 shards", 16 << 20, [256], 0.10, 4,
+           0x5EED0003, "c3_256B_10pct_invalid_n4"),
+    "c4": ("C4: 16 MiB batches of 1024-byte metrics, 16 downstream shards", 16 << 20, [1024], 0.0, 16, 0x5EED0004,
+           "c4_1024B_n16"),
+    "c5": ("C5: 16 MiB batches of mixed 64/256/1024-byte metrics, 64 shards", 16 << 20, [64, 256, 1024], 0.0, 64,
+           0x5EED0005, "c5_mixed_n64"),
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=4096)
-    ap.add_argument("--warmup", type=int, default=2048,
-                    help="untimed steps first (about 12 ms at C2: the clocks settle)")
+    ap.add_argument("--steps", type=int, default=200, help="timed launches (32 x 16 MiB batches each)")
+    ap.add_argument("--warmup", type=int, default=20, help="untimed launches first")
+    ap.add_argument("--min-warmup-ms", type=float, default=60.0,
+                    help="keep warming up until this much time has passed (clocks settle)")
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--batches", type=int, default=64, help="distinct batches in the rotating set")
-    ap.add_argument("--per-launch", type=int, default=32,
-                    help="batches routed per kernel launch (sr_route_device_many; 1 = sr_route_device)")
-    ap.add_argument("--dead", type=float, default=0.0, help="fraction of dead downstreams")
+    ap.add_argument("--per-launch", type=int, default=32, help="batches per route_kernel launch (one step)")
+    ap.add_argument("--dead", type=float, default=0.0,
+                    help="fraction of dead downstreams (0.25 uses the digest's alive mask)")
     ap.add_argument("--regroup", default="auto", choices=["auto", "on", "off"],
                     help="classify + all-to-all regroup leg (auto: on when more than one GPU)")
+    ap.add_argument("--regroup-config", default="c5", choices=sorted(CONFIGS))
     ap.add_argument("--regroup-steps", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--dry-ranks", action="store_true",
+                    help="each rank prints its RANK / LOCAL_RANK / WORLD_SIZE and exits (launcher test; no GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(args_argv, n):
+    """torch.distributed.run command line re-running this script with N ranks (one per GPU)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+            os.path.abspath(__file__)] + list(args_argv)
+
+
+def maybe_spawn(args, argv) -> int | None:
+    """--gpus N > 1 outside a torch.distributed launch: start the N ranks as child processes
+    (before this process touches the GPU) and return their exit code. None = run here."""
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if args.gpus not in (1, world):
+            raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+        return None
+    if args.gpus <= 1:
+        return None
+    return subprocess.run(launcher_cmd(argv, args.gpus)).returncode
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    rc = maybe_spawn(args, argv)
+    if rc is not None:
+        sys.exit(rc)
+    if args.dry_ranks:
+        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}),
+              flush=True)
+        return
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
     # The contract is ONE JSON line on stdout. Libraries (RCCL's version banner, HIP runtime notes)
     # write to fd 1 as well: point fd 1 at stderr and keep a private handle for the result line.
     json_out = os.fdopen(os.dup(1), "w")
@@ -77,27 +146,33 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pkg = importlib.import_module("statsd-router_amd")
+    digests = json.load(open(os.path.join(REPO, "tests", "golden", "digests.json")))
 
-    desc, batch_bytes, lens, p_inv, shards, seed0 = CONFIGS[args.config]
-    rng = np.random.default_rng(seed0 + 7919 * rank)
-    alive = [1] * shards
+    desc, batch_bytes, lens, p_inv, shards, seed0, dkey = CONFIGS[args.config]
+    alive, alive_tag = [1] * shards, "all"
     if args.dead > 0:
-        for k in rng.choice(shards, max(1, int(round(args.dead * shards))), replace=False):
-            alive[int(k)] = 0
+        alive_tag = "dead25" if abs(args.dead - 0.25) < 1e-9 else None
+        if alive_tag and f"{dkey}/{alive_tag}" in digests:
+            words = [int(w, 16) for w in digests[f"{dkey}/{alive_tag}"]["alive"]]
+            alive = [(words[k >> 6] >> (k & 63)) & 1 for k in range(shards)]
+        else:
+            rng = np.random.default_rng(seed0 + 7919 * rank)
+            for k in rng.choice(shards, max(1, int(round(args.dead * shards))), replace=False):
+                alive[int(k)] = 0
 
     # ---- rotating set of distinct batches, resident in HBM -------------------------------------
     B = args.batches
-    host = []
-    for b in range(B):
-        s = pkg.gen_stream(batch_bytes, lens, seed=seed0 + 1_000_003 * rank + 65_537 * b, p_invalid=p_inv)
-        host.append(s)
+    M = max(1, min(args.per_launch, pkg.SR_MAX_BATCHES_PER_LAUNCH, B))
+    B -= B % M                                  # whole launches only
+    ng = B // M                                 # launch groups in the rotating set
+    host = [pkg.gen_stream(batch_bytes, lens, seed=seed0 + 1_000_003 * rank + 65_537 * b, p_invalid=p_inv)
+            for b in range(B)]
     sizes = [int(s.data.size) for s in host]
     lines = [int(s.n_lines) for s in host]
     d_in = torch.empty((B, batch_bytes), dtype=torch.uint8, device=dev)
     for b, s in enumerate(host):
         d_in[b, : sizes[b]].copy_(torch.from_numpy(s.data))
     max_lines = max(lines)
-    M = max(1, min(args.per_launch, pkg.SR_MAX_BATCHES_PER_LAUNCH, B))
     # one record array per batch slot of a launch (batches of one launch never share records)
     d_out = torch.empty((M, max_lines * 8), dtype=torch.uint8, device=dev)
     d_cnt = torch.zeros(B, dtype=torch.int64, device=dev)
@@ -107,37 +182,32 @@ def main():
     router.set_stream(stream.cuda_stream)
     in_ptr, out_ptr, cnt_ptr = d_in.data_ptr(), d_out.data_ptr(), d_cnt.data_ptr()
 
-    def launch_range(i0, i1):
-        """Steps i0 .. i1-1 (batch i % B each), M batches per kernel launch."""
-        for j0 in range(i0, i1, M):
-            descs = []
-            for m, i in enumerate(range(j0, min(j0 + M, i1))):
-                b = i % B
-                descs.append((in_ptr + b * batch_bytes, sizes[b], out_ptr + m * max_lines * 8, max_lines, None,
-                              cnt_ptr + 8 * b))
-            if M == 1:
-                router.route_device(*descs[0])
-            else:
-                router.route_device_many(descs)
+    def launch(gi):
+        """One step: launch group gi (batches gi*M .. gi*M+M-1) in ONE route_kernel launch."""
+        router.route_device_many([(in_ptr + b * batch_bytes, sizes[b], out_ptr + m * max_lines * 8, max_lines, None,
+                                   cnt_ptr + 8 * b) for m, b in enumerate(range(gi * M, gi * M + M))])
 
-    def launch(i):   # one launch: steps i*M .. i*M+M-1
-        launch_range(i * M, i * M + M)
-
+    group_bytes = [sum(sizes[gi * M: gi * M + M]) for gi in range(ng)]
+    group_lines = [sum(lines[gi * M: gi * M + M]) for gi in range(ng)]
+    K = max(1, args.steps)
     with torch.cuda.stream(stream):
-        launch_range(0, max(args.warmup, 1))
+        for gi in range(ng):                    # eager once (allocations, code load)
+            launch(gi)
         stream.synchronize()
-        # capture the rotating set as one graph (+ a tail graph so exactly K steps are timed)
-        K = args.steps
-        g_full = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_full, stream=stream):
-            launch_range(0, B)
-        g_tail = None
-        if K % B:
-            g_tail = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g_tail, stream=stream):
-                launch_range(0, K % B)
-        g_full.replay()
-        stream.synchronize()
+        graphs = []
+        for gi in range(ng):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=stream):
+                launch(gi)
+            graphs.append(g)
+        # warm-up: W launches, and at least --min-warmup-ms of back-to-back launches
+        t_w = time.perf_counter()
+        w_done = 0
+        while w_done < args.warmup or (time.perf_counter() - t_w) * 1e3 < args.min_warmup_ms:
+            for _ in range(16):
+                graphs[w_done % ng].replay()
+                w_done += 1
+            stream.synchronize()
 
         # ---- timed region: exactly K steps ------------------------------------------------------
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -146,10 +216,8 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ev0.record(stream)
-        for _ in range(K // B):
-            g_full.replay()
-        if g_tail is not None:
-            g_tail.replay()
+        for i in range(K):
+            graphs[i % ng].replay()
         ev1.record(stream)
         torch.cuda.synchronize()
         if world > 1:
@@ -157,25 +225,14 @@ def main():
         t1 = time.perf_counter()
         region_ms = ev0.elapsed_time(ev1)
 
-        # per-launch durations (HIP events on the launch stream), outside the timed region
-        nprobe = max(1, min(K, 512) // M)
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nprobe)]
-        probe_bytes = 0
-        for i, (a, z) in enumerate(evs):
-            a.record(stream)
-            launch(i)
-            z.record(stream)
-            probe_bytes += sum(sizes[j % B] for j in range(i * M, i * M + M))
-        stream.synchronize()
-        launch_ms = float(np.mean([a.elapsed_time(z) for a, z in evs]))
-        bytes_per_launch = probe_bytes / nprobe
-
     counts = d_cnt.cpu().numpy()
     assert all(int(counts[b]) == lines[b] for b in range(B)), "line counts differ from the generator"
+    verify = None if args.no_verify else verify_timed_launch(pkg, graphs[0], stream, d_out, host, M, max_lines,
+                                                             shards, alive, rank, digests, dkey, alive_tag)
 
     wall = t1 - t0
-    steps_lines = sum(lines[i % B] for i in range(K))
-    steps_bytes = sum(sizes[i % B] for i in range(K))
+    steps_lines = sum(group_lines[i % ng] for i in range(K))
+    steps_bytes = sum(group_bytes[i % ng] for i in range(K))
     t = torch.tensor([wall, region_ms / 1e3], dtype=torch.float64, device=dev)
     tot = torch.tensor([steps_lines, steps_bytes], dtype=torch.float64, device=dev)
     if world > 1:
@@ -186,7 +243,9 @@ def main():
 
     result = None
     if rank == 0:
-        achieved = bytes_per_launch / (launch_ms * 1e-3) / 1e9
+        # the dominant kernel's achieved HBM rate: algorithmic bytes (the framed bytes, read once)
+        # of the timed launches on this GPU over their GPU time
+        achieved = steps_bytes / (region_ms * 1e-3) / 1e9
         traffic = None
         tj = args.traffic_json
         if tj and os.path.exists(tj):
@@ -201,14 +260,16 @@ def main():
             "n_gpus": world,
             "steps": K,
             "warmup": args.warmup,
+            "warmup_launches_run": w_done,
             "ms_per_step": round(wall_max * 1e3 / K, 6),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u64",
-            "data": f"synthetic: seeded sr_gen streams, {B} distinct framed batches per GPU resident in HBM",
+            "data": f"synthetic: seeded sr_gen streams, {B} distinct framed 16 MiB batches per GPU resident in HBM",
             "config": {
                 "workload": desc,
+                "step": f"one route_kernel launch over {M} distinct batches ({group_bytes[0]} B at group 0)",
                 "batch_bytes": batch_bytes,
                 "line_bytes": lens,
                 "p_invalid": p_inv,
@@ -217,7 +278,7 @@ def main():
                 "rotating_batches": B,
                 "parallelism": f"dp{world} (independent datagram batches per GPU)",
                 "batches_per_launch": M,
-                "launch": f"hipGraph replay of back-to-back route_kernel launches, {M} batches each",
+                "launch": f"hipGraph replay, one graph per launch of {M} batches, {ng} graphs alternating",
             },
             "gib_per_s": round(total_bytes / wall_max / 2**30, 3),
             "gpu_region_ms": round(region_max * 1e3, 4),
@@ -229,84 +290,145 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "kernel": "route_kernel",
-                "bytes_per_launch": bytes_per_launch,
-                "launch_us": round(launch_ms * 1e3, 3),
-                "launch_timing": f"mean of {nprobe} eager launches ({M} batches each), each bracketed by HIP events "
-                                 "on its stream",
+                "bytes_per_launch": steps_bytes / K,
+                "launch_us": round(region_ms * 1e3 / K, 3),
+                "launch_timing": (f"timed region: {K} back-to-back launches between two HIP events on the launch "
+                                  "stream; achieved = the region's framed bytes / the region's event time"),
             },
+            "verify": verify,
             "cpu_baseline": None,
         }
 
         if world == 1 and not args.no_cpu:
-            sys.path.insert(0, os.path.join(REPO, "oracle"))
-            import sr_oracle
-
-            sample = [host[b].data for b in range(min(4, B))]
-            cores = min(16, os.cpu_count() or 1)
-            l1, b1, w1 = sr_oracle.bench(sample, shards, alive, 1, args.cpu_seconds)
-            lm, bm, wm = sr_oracle.bench(sample, shards, alive, cores, args.cpu_seconds)
-            result["cpu_baseline"] = {
-                "value": round(lm / wm / 1e6, 3),
-                "unit": "M metrics/s",
-                "cores": cores,
-                "kind": "port",
-                "sample": (f"{len(sample)} x 16 MiB batches of the same workload routed repeatedly by the C "
-                           f"restatement (oracle/sr_oracle.c: memchr + serial sdbm + probe, like sr-main.c:175-189), "
-                           f"{cores} threads x {args.cpu_seconds:.1f} s"),
-                "single_thread": round(l1 / w1 / 1e6, 3),
-                "single_thread_gib_per_s": round(b1 / w1 / 2**30, 3),
-                "gib_per_s": round(bm / wm / 2**30, 3),
-            }
-
+            result["cpu_baseline"] = cpu_baseline(host, shards, alive, args.cpu_seconds)
         if not args.no_e2e:
             result["e2e"] = e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M)
+    router.close()
+    del d_in, d_out
+    torch.cuda.empty_cache()
     if args.regroup == "on" or (args.regroup == "auto" and world > 1):
-        rg = regroup_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, B, max_lines, dev, world,
-                         args.regroup_steps)
+        rg = regroup_leg(pkg, dev, local, world, rank, args.regroup_config, args.regroup_steps)
         if rank == 0:
             result["regroup"] = rg
-    router.close()
     if rank == 0:
         print(json.dumps(result), file=json_out, flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 
 
-def regroup_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, B, max_lines, dev, world, steps):
-    """Classify + regroup: per batch, route, pack by owner GPU (shard % G) and
-    all-to-all the packed lines and records (RCCL over xGMI). Not graph-captured: the split sizes
-    go through the host. Timed like the main region (barrier + synchronize, max over ranks)."""
+def verify_timed_launch(pkg, graph, stream, d_out, host, M, max_lines, shards, alive, rank, digests, dkey, tag):
+    """Replay launch 0 of the timed set once more; batch 0's records against the reference digest
+    (rank 0: same seed as tests/golden/digests.json), the last batch of the launch against the
+    oracle record for record. Raises on any difference."""
+    import numpy as np
+
+    graph.replay()
+    stream.synchronize()
+    out = {}
+    n0 = host[0].n_lines
+    r0 = d_out[0, : n0 * 8].cpu().numpy().tobytes()
+    key = f"{dkey}/{tag}" if tag else None
+    if rank == 0 and key in digests and digests[key]["nbytes"] == host[0].data.size:
+        want = digests[key]["sha256_records"]
+        got = hashlib.sha256(r0).hexdigest()
+        if got != want:
+            raise SystemExit(f"batch 0 records differ from the reference digest {key}: {got} != {want}")
+        out["digest"] = f"{key}: batch 0 records sha256 match the compiled reference"
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import sr_oracle
+
+    m = M - 1
+    crecs, _, cn = sr_oracle.route(host[m].data, shards, alive)
+    got = np.frombuffer(d_out[m, : cn * 8].cpu().numpy().tobytes(), dtype=pkg.RECORD_DTYPE)
+    if cn != host[m].n_lines or not np.array_equal(got, crecs):
+        raise SystemExit(f"batch {m} of the timed launch differs from the oracle")
+    out["oracle"] = f"batch {m} of launch 0 ({cn} lines) equals the C oracle record for record"
+    return out
+
+
+def cpu_baseline(host, shards, alive, seconds):
+    """The C restatement (oracle/sr_oracle.c, calibrated against the compiled reference in
+    BASELINE.md) routing the same batches on this host: 1 thread, and one thread per CPU of the
+    process's share, each thread one reference data thread (threads_num, sr-main.c:363-367)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import sr_oracle
+
+    sample = [host[b].data for b in range(min(4, len(host)))]
+    affinity = len(os.sched_getaffinity(0))
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    cores = min(affinity, share) if share > 0 else affinity
+    l1, b1, w1 = sr_oracle.bench(sample, shards, alive, 1, seconds)
+    lm, bm, wm = sr_oracle.bench(sample, shards, alive, cores, seconds)
+    return {
+        "value": round(lm / wm / 1e6, 3),
+        "unit": "M metrics/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": (f"{len(sample)} x 16 MiB batches of the same workload routed repeatedly by the C restatement "
+                   f"(oracle/sr_oracle.c: memchr + serial sdbm + probe, like sr-main.c:175-189), "
+                   f"{cores} threads x {seconds:.1f} s = {cores * seconds:.0f} core-seconds"),
+        "single_thread": round(l1 / w1 / 1e6, 3),
+        "single_thread_gib_per_s": round(b1 / w1 / 2**30, 3),
+        "gib_per_s": round(bm / wm / 2**30, 3),
+        "cpu_model": cpu_model(),
+        "host_cpus": os.cpu_count(),
+        "cores_note": (f"threads = the process's CPU share (sched_getaffinity {affinity}, OMP_NUM_THREADS "
+                       f"{share or 'unset'}); on the GPU box that share is 16 CPUs per GPU"),
+    }
+
+
+def regroup_leg(pkg, dev, local, world, rank, cfg, steps):
+    """Classify + regroup on its own batches of config `cfg` (C5 by default: mixed
+    lengths, 64 shards): per batch, route, pack by owner GPU (shard % G) and all-to-all the packed
+    lines and records (RCCL over xGMI). Not graph-captured: the split sizes go through the host.
+    Timed like the main region (barrier + synchronize, max over ranks)."""
+    import torch
+    import torch.distributed as dist
+
     rg_mod = importlib.import_module("statsd-router_amd.regroup")
     if world == 1 and not dist.is_initialized():
         dist.init_process_group("nccl", store=dist.TCPStore("127.0.0.1", 0, 1, True), rank=0, world_size=1)
-    reg = rg_mod.Regrouper(pkg, router, batch_bytes, max_lines, slots=2)
+    desc, batch_bytes, lens, p_inv, shards, seed0, _ = CONFIGS[cfg]
+    nb = 4
+    host = [pkg.gen_stream(batch_bytes, lens, seed=seed0 + 1_000_003 * rank + 65_537 * b, p_invalid=p_inv)
+            for b in range(nb)]
+    sizes = [int(s.data.size) for s in host]
+    lines = [int(s.n_lines) for s in host]
+    max_lines = max(lines)
+    d_in = torch.empty((nb, batch_bytes), dtype=torch.uint8, device=dev)
+    for b, s in enumerate(host):
+        d_in[b, : sizes[b]].copy_(torch.from_numpy(s.data))
+    stream = torch.cuda.Stream(device=dev)
+    router = pkg.Router(shards, batch_bytes, device=local)
+    router.set_stream(stream.cuda_stream)
     d_rec = torch.empty(max_lines, dtype=torch.int64, device=dev)
     d_n = torch.zeros(1, dtype=torch.int64, device=dev)
     base = d_in.data_ptr()
-    rank = dist.get_rank()
-
-    def start(i):
-        b = i % B
-        router.route_device(base + b * batch_bytes, sizes[b], d_rec.data_ptr(), max_lines, None, d_n.data_ptr())
-        reg.start(i % 2, base + b * batch_bytes, sizes[b], d_rec.data_ptr(), d_n.data_ptr(), max_lines)
-
-    def finish(i):
-        rb, rr, _ = reg.finish(i % 2)
-        # bytes this rank sent to the other ranks, from the host copy the exchange already made
-        sent = sum(c[1] for c in reg.last_sent) - reg.last_sent[rank][1]
-        return int(rr.numel()), int(rb.numel()), sent
-
-    def run(n):
-        # two slots: batch i+1 is routed and packed while the host waits for batch i's split sizes
-        acc = [0, 0, 0]
-        start(0)
-        for i in range(n):
-            if i + 1 < n:
-                start(i + 1)
-            acc = [a + x for a, x in zip(acc, finish(i))]
-        return acc
 
     with torch.cuda.stream(stream):
+        reg = rg_mod.Regrouper(pkg, router, batch_bytes, max_lines, slots=2)
+
+        def start(i):
+            b = i % nb
+            router.route_device(base + b * batch_bytes, sizes[b], d_rec.data_ptr(), max_lines, None, d_n.data_ptr())
+            reg.start(i % 2, base + b * batch_bytes, sizes[b], d_rec.data_ptr(), d_n.data_ptr(), max_lines)
+
+        def finish(i):
+            rb, rr, _ = reg.finish(i % 2)
+            # bytes this rank sent to the other ranks, from the host copy the exchange already made
+            sent = sum(c[1] for c in reg.last_sent) - reg.last_sent[rank][1]
+            return int(rr.numel()), int(rb.numel()), sent
+
+        def run(n):
+            # two slots: batch i+1 is routed and packed while the host waits for batch i's split sizes
+            acc = [0, 0, 0]
+            start(0)
+            for i in range(n):
+                if i + 1 < n:
+                    start(i + 1)
+                acc = [a + x for a, x in zip(acc, finish(i))]
+            return acc
+
         run(2)
         torch.cuda.synchronize()
         dist.barrier()
@@ -315,13 +437,14 @@ def regroup_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, B, max_lin
         torch.cuda.synchronize()
         dist.barrier()
         wall = time.perf_counter() - t0
+    router.close()
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    tot = torch.tensor([sum(lines[i % B] for i in range(steps)), recv_lines, recv_bytes, sent_off],
+    tot = torch.tensor([sum(lines[i % nb] for i in range(steps)), recv_lines, recv_bytes, sent_off],
                        dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     w = float(t[0])
-    return {"value": round(float(tot[0]) / w / 1e6, 3), "unit": "M metrics/s",
+    return {"value": round(float(tot[0]) / w / 1e6, 3), "unit": "M metrics/s", "workload": desc,
             "steps_per_gpu": steps, "ms_per_step": round(w * 1e3 / steps, 4),
             "lines_regrouped": int(tot[1]), "bytes_regrouped": int(tot[2]),
             "bytes_sent_to_other_gpus_per_s": round(float(tot[3]) / w / 1e9, 3),
@@ -336,6 +459,8 @@ def e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M, groups=24)
     Groups of M batches, double-buffered: the H2D copy of group g+1 (copy stream) overlaps the
     route launch of group g (the context's stream, M batches per launch as in the timed region)
     and the D2H of group g-1's records (third stream)."""
+    import torch
+
     nb = min(len(host), 2 * M)
     pinned = [torch.from_numpy(host[b].data).pin_memory() for b in range(nb)]
     max_lines = max(lines)

@@ -101,6 +101,14 @@ int sr_set_stream(sr_ctx *ctx, void *stream);
 int sr_route_batch(sr_ctx *ctx, const uint8_t *bytes, size_t nbytes, sr_record *out,
                    size_t max_records, size_t *n_records, uint64_t *hashes);
 
+/* The dead-downstream side effect of the last sr_route_batch call: find_downstream zeroes
+ * active_buffer_length of every DEAD downstream its probe visits (sr-main.c:106). With the batch's
+ * alive snapshot a dead downstream receives no line in that batch, so the caller reproduces the
+ * effect exactly by dropping the pending buffer of every downstream whose bit is set here, before
+ * it pushes the batch's lines. Writes ceil(n_downstreams/64) words (none when n_downstreams == 0).
+ * Returns 0 or -EINVAL. */
+int sr_last_probed_dead(const sr_ctx *ctx, uint64_t *bitmap);
+
 /* Device-resident batch (asynchronous, enqueued on the context's stream): d_bytes, d_out,
  * d_hashes (may be NULL) and d_n_records are device pointers. Lines past max_records are counted
  * but not written; the line count is stored to *d_n_records when the work completes.
@@ -121,6 +129,9 @@ typedef struct sr_batch {
     size_t max_records;
     uint64_t *d_hashes;      /* NULL or max_records u64, device memory                  */
     uint64_t *d_n_records;   /* device u64: the batch's line count                      */
+    uint64_t *d_probed_dead; /* NULL, or max(1, ceil(n_downstreams/64)) device u64: bit k  */
+                             /* set iff some line of the batch probed dead downstream k   */
+                             /* (find_downstream zeroes its active buffer, sr-main.c:106) */
 } sr_batch;
 int sr_route_device_many(sr_ctx *ctx, const sr_batch *batches, size_t count);
 
@@ -132,7 +143,8 @@ int sr_route_device_many(sr_ctx *ctx, const sr_batch *batches, size_t count);
  * receives {lines, bytes} per owner (2*n_owners u64: the all-to-all split sizes). Lines routed
  * to no shard are not packed (their WARN stays with the GPU that received them).
  * d_recs / d_n_records: the output of sr_route_device for the same batch (same stream).
- * out_cap >= SR_PACK_CAPACITY(nbytes) guarantees room; d_out_recs needs max_records entries.
+ * out_cap must be >= SR_PACK_CAPACITY(nbytes) (else -EINVAL), and SR_PACK_CAPACITY(nbytes) must fit
+ * 32 bits (nbytes up to ~2.8 GB); d_out_recs needs max_records entries.
  * Asynchronous on the context's stream. n_owners in 1..64. Returns 0, -EINVAL, -ENOMEM, -EIO.
  * The first call (or one with a larger max_records / n_owners) allocates scratch: not inside
  * stream capture. */

@@ -173,7 +173,7 @@ struct DeviceState {
     }
 
     static bool add_batch(RouteParams &p, const uint8_t *d_bytes, size_t nbytes, sr_record *d_out,
-                          size_t max_records, uint64_t *d_hashes, uint64_t *d_n) {
+                          size_t max_records, uint64_t *d_hashes, uint64_t *d_n, uint64_t *d_probed_dead = nullptr) {
         if (p.nb >= (uint32_t)kMaxBatches) return false;
         BatchDesc &b = p.b[p.nb++];
         b.bytes = d_bytes;
@@ -182,7 +182,8 @@ struct DeviceState {
         b.hashes = d_hashes;
         b.n_out = d_n;
         b.max_records = (uint32_t)(max_records > 0xFFFFFFFFull ? 0xFFFFFFFFull : max_records);
-        b.tile0 = b.ntiles = b.sbase = b.cls = 0;
+        b.tile0 = b.ntiles = b.sbase = b.cls = b.pad = 0;
+        b.probed_dead = d_probed_dead;
         return true;
     }
 
@@ -208,11 +209,20 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
     RouteParams p = in;
     p.nb = 0;
     for (uint32_t i = 0; i < in.nb; ++i) {
+        // the probed-dead bitmap starts empty; with every shard alive nothing can set it
+        if (in.b[i].probed_dead) {
+            if (hipMemsetAsync(in.b[i].probed_dead, 0, (size_t)(ds.nwords ? ds.nwords : 1) * sizeof(uint64_t),
+                               stream) != hipSuccess)
+                return -EIO;
+        }
+    }
+    for (uint32_t i = 0; i < in.nb; ++i) {
         if (in.b[i].nbytes == 0) {
             if (hipMemsetAsync(in.b[i].n_out, 0, sizeof(uint64_t), stream) != hipSuccess) return -EIO;
             continue;
         }
         p.b[p.nb++] = in.b[i];
+        if (ds.dead == 0) p.b[p.nb - 1].probed_dead = nullptr;
     }
     if (p.nb == 0) return 0;
     // 8+ batches: each batch's tiles on one XCD class; its scanner (block j) shares that class

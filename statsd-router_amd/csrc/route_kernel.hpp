@@ -143,6 +143,9 @@ struct BatchDesc {
     uint32_t ntiles;
     uint32_t sbase;          // first status / base granule of the batch
     uint32_t cls;            // XCD class: the tiles of the batch are blocks nb + cls + 8 i
+    uint32_t pad;
+    uint64_t *probed_dead;   // may be null: bit k set = dead shard k was probed by some line
+                             // (find_downstream zeroes its active buffer, sr-main.c:106)
 };
 
 struct RouteParams {
@@ -465,11 +468,34 @@ __device__ __forceinline__ bool alive_bit(const uint64_t *alive, uint32_t k) {
     return (alive[k >> 6] >> (k & 63)) & 1ull;
 }
 
+// Bit k of the batch's probed-dead bitmap: the reference zeroes the active buffer of every dead
+// downstream it probes (sr-main.c:106). Read first, so that once a bit is set (after the first few
+// lines) the line costs an L2 read and no same-address atomic.
+__device__ __forceinline__ void note_dead(uint64_t *pd, uint32_t k) {
+    uint64_t *w = pd + (k >> 6);
+    const uint64_t bit = 1ull << (k & 63);
+    if (!(__hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & bit))
+        __hip_atomic_fetch_or(w, bit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Every shard dead: each routed line probes all n positions of the permutation, i.e. every shard.
+__device__ __noinline__ void note_all_dead(uint64_t *pd, uint32_t n) {
+    for (uint32_t w = 0; w < (n + 63) / 64; ++w) {
+        const uint64_t full = (w + 1) * 64 <= n ? ~0ull : ((1ull << (n & 63)) - 1ull);
+        if ((__hip_atomic_load(pd + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & full) != full)
+            __hip_atomic_fetch_or(pd + w, full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
 // find_downstream (sr-main.c:86-117) for one line. Returns the shard, SR_ROUTE_ALL_DEAD, or
-// kRoutePending if more than kOverlay dead shards had to be probed.
-__device__ uint32_t probe_shard(uint64_t h, const RouteParams &p) {
+// kRoutePending if more than kOverlay dead shards had to be probed. pd (may be null): the batch's
+// probed-dead bitmap.
+__device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *pd) {
     const uint32_t n = p.nds;
-    if (p.dead >= n) return SR_ROUTE_ALL_DEAD;            // includes N == 0
+    if (p.dead >= n) {                                    // includes N == 0
+        if (pd && n) note_all_dead(pd, n);
+        return SR_ROUTE_ALL_DEAD;
+    }
     if (p.dead == 0) return mod_magic(h, p.magic_n, n);   // every shard alive: j = h % N
     // ds_index[] is the identity plus an overlay of (position -> value) writes, newest last.
     uint32_t ov[kOverlay];   // (pos << 16) | value
@@ -484,6 +510,7 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p) {
         for (int e = 0; e < kOverlay; ++e)
             if ((ov[e] >> 16) == j) k = ov[e] & 0xFFFFu;
         if (alive_bit(p.alive, k)) return k;                         // :101-104
+        if (pd) note_dead(pd, k);                                    // :106
         if (j != i - 1) {                                            // :108-111
             uint32_t v = i - 1;
 #pragma unroll
@@ -1289,7 +1316,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     uint32_t route;
                     if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
                     else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
-                    else route = probe_shard(h, p);                                                    // :145
+                    else route = probe_shard(h, p, bd.probed_dead);                                    // :145
                     sr_record r;
                     r.offset = (uint32_t)(T0 + s);
                     r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
@@ -1518,6 +1545,7 @@ __global__ __launch_bounds__(64) void probe_wide_kernel(RouteParams p) {
             const uint32_t k = ds_index[j];
             ++steps;
             if (alive_bit(p.alive, k)) { route = k; break; }
+            if (p.b[pl.batch].probed_dead) note_dead(p.b[pl.batch].probed_dead, k);   // :106
             if (j != i - 1) {
                 ds_index[j] = ds_index[i - 1];
                 ds_index[i - 1] = (uint16_t)k;

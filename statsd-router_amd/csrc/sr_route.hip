@@ -32,54 +32,44 @@ struct sr_ctx {
     uint64_t *d_hash;
     size_t d_hash_cap;
     uint64_t *d_count;
+    uint64_t *d_probed;           // probed-dead bitmap of the host-memory path
+    uint64_t *h_probed;           // its copy after the last sr_route_batch
     // scratch of sr_pack_by_owner
     uint2 *d_pack_tiles;          // tile counts | tile bases
     size_t pack_tiles_cap;        // entries per array
     uint64_t *d_owner_start;
 };
 
-// The product instantiation is ABL_NONE. SR_VARIANT in the environment selects one of a few
-// compiled-in variants instead, for same-box A/B measurements with bench.py:
-// v05 = the round-1 v0.5 components (hash, masks, serial scanner, late base read, sc1-only granules).
+// The product launches exactly one instantiation, ABL_NONE. Ablation variants (records wrong by
+// design in some of them) exist only in builds made with -DSR_ABLATION_VARIANTS (`make VARIANTS=1`,
+// developer A/B runs; never the shipped library): SR_VARIANT in the environment then selects one.
+#ifdef SR_ABLATION_VARIANTS
 static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream_t stream) {
     static const int v = [] {
         const char *e = getenv("SR_VARIANT");
         if (!e || !*e) return 0;
-        if (!strcmp(e, "early_base")) return 1;
-        if (!strcmp(e, "old_scanner")) return 3;
-        if (!strcmp(e, "old_hash")) return 4;
-        if (!strcmp(e, "old_masks")) return 5;
-        if (!strcmp(e, "v05")) return 6;
-        if (!strcmp(e, "agent_granules")) return 11;
-        if (!strcmp(e, "scan_serial")) return 12;
         if (!strcmp(e, "mixed_lanes")) return 13;
         if (!strcmp(e, "no_mid_base")) return 14;
         // upper bounds, not routing (records wrong or missing; line counts still exact)
         if (!strcmp(e, "fake_base")) return 7;
         if (!strcmp(e, "no_hash")) return 8;
         if (!strcmp(e, "no_lines")) return 9;
-        if (!strcmp(e, "fake_base_no_hash")) return 10;
         return 0;
     }();
     switch (v) {
-    case 1: return launch_route<kBlock, ABL_EARLY_BASE>(ds, p, stream);
-    case 3: return launch_route<kBlock, ABL_OLD_SCANNER>(ds, p, stream);
-    case 4: return launch_route<kBlock, ABL_OLD_HASH>(ds, p, stream);
-    case 5: return launch_route<kBlock, ABL_OLD_MASKS>(ds, p, stream);
-    case 6:
-        return launch_route<kBlock, ABL_OLD_HASH | ABL_OLD_MASKS | ABL_OLD_SCANNER | ABL_AGENT_GRANULES | ABL_SCAN_SERIAL>(
-            ds, p, stream);
-    case 11: return launch_route<kBlock, ABL_AGENT_GRANULES>(ds, p, stream);
-    case 12: return launch_route<kBlock, ABL_SCAN_SERIAL>(ds, p, stream);
     case 13: return launch_route<kBlock, ABL_MIXED_LANES>(ds, p, stream);
     case 14: return launch_route<kBlock, ABL_NO_MID_BASE>(ds, p, stream);
     case 7: return launch_route<kBlock, ABL_FAKE_BASE>(ds, p, stream);
     case 8: return launch_route<kBlock, ABL_NO_HASH>(ds, p, stream);
     case 9: return launch_route<kBlock, ABL_NO_LINES>(ds, p, stream);
-    case 10: return launch_route<kBlock, ABL_FAKE_BASE | ABL_NO_HASH>(ds, p, stream);
     default: return launch_route<kBlock, ABL_NONE>(ds, p, stream);
     }
 }
+#else
+static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream_t stream) {
+    return launch_route<kBlock, ABL_NONE>(ds, p, stream);
+}
+#endif
 
 extern "C" {
 
@@ -117,6 +107,8 @@ void sr_close(sr_ctx *c) {
     (void)hipFree(c->d_out);
     (void)hipFree(c->d_hash);
     (void)hipFree(c->d_count);
+    (void)hipFree(c->d_probed);
+    free(c->h_probed);
     (void)hipFree(c->d_pack_tiles);
     (void)hipFree(c->d_owner_start);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -142,6 +134,8 @@ int sr_open(sr_ctx **out, int device, size_t max_batch_bytes, uint32_t n_downstr
     rc = -ENOMEM;
     if (hipMalloc(&c->d_in, max_batch_bytes) != hipSuccess) goto fail;
     if (hipMalloc(&c->d_count, sizeof(uint64_t)) != hipSuccess) goto fail;
+    if (hipMalloc(&c->d_probed, (c->ds.nwords ? c->ds.nwords : 1) * sizeof(uint64_t)) != hipSuccess) goto fail;
+    if (!(c->h_probed = (uint64_t *)calloc(c->ds.nwords ? c->ds.nwords : 1, sizeof(uint64_t)))) goto fail;
     *out = c;
     return 0;
 fail:
@@ -167,6 +161,12 @@ int sr_sync(sr_ctx *c) {
     return hipStreamSynchronize(c->stream) == hipSuccess ? 0 : -EIO;
 }
 
+int sr_last_probed_dead(const sr_ctx *c, uint64_t *bitmap) {
+    if (!c || (!bitmap && c->ds.nwords)) return -EINVAL;
+    if (c->ds.nwords) memcpy(bitmap, c->h_probed, c->ds.nwords * sizeof(uint64_t));
+    return 0;
+}
+
 int sr_route_device(sr_ctx *c, const uint8_t *d_bytes, size_t nbytes, sr_record *d_out, size_t max_records,
                     uint64_t *d_hashes, uint64_t *d_n_records) {
     if (!c || !d_n_records || (nbytes && !d_bytes) || nbytes > c->ds.max_batch) return -EINVAL;
@@ -189,7 +189,7 @@ int sr_route_device_many(sr_ctx *c, const sr_batch *batches, size_t count) {
         RouteParams p = c->ds.params();
         for (size_t i = i0; i < count && i < i0 + kMaxBatches; ++i)
             DeviceState::add_batch(p, batches[i].d_bytes, batches[i].nbytes, batches[i].d_out, batches[i].max_records,
-                                   batches[i].d_hashes, batches[i].d_n_records);
+                                   batches[i].d_hashes, batches[i].d_n_records, batches[i].d_probed_dead);
         const int rc = launch_variant(c->ds, p, c->stream);
         if (rc) return rc;
     }
@@ -200,7 +200,11 @@ int sr_pack_by_owner(sr_ctx *c, const uint8_t *d_bytes, size_t nbytes, const sr_
                      const uint64_t *d_n_records, size_t max_records, uint32_t n_owners, uint8_t *d_out_bytes,
                      size_t out_cap, sr_record *d_out_recs, uint64_t *d_owner_counts) {
     if (!c || !d_n_records || !d_owner_counts || n_owners == 0 || n_owners > SR_MAX_OWNERS) return -EINVAL;
-    if (nbytes > 0xFFFFFFF0ull || max_records > 0xFFFFFFFFull || out_cap > 0xFFFFFFFFull) return -EINVAL;
+    // the packed layout is addressed with u32 offsets: its worst case must fit 32 bits, and the
+    // caller's buffer must hold that worst case (the kernels never truncate silently)
+    if (max_records > 0xFFFFFFFFull || SR_PACK_CAPACITY((uint64_t)nbytes) > 0xFFFFFFFFull) return -EINVAL;
+    if (out_cap < SR_PACK_CAPACITY((uint64_t)nbytes)) return -EINVAL;
+    if (out_cap > 0xFFFFFFFFull) out_cap = 0xFFFFFFFFull;
     if (max_records && (!d_recs || !d_out_recs || !d_bytes || !d_out_bytes)) return -EINVAL;
     (void)hipSetDevice(c->device);
     const uint32_t ntiles = (uint32_t)((max_records + kPackTile - 1) / kPackTile);
@@ -247,8 +251,13 @@ int sr_route_batch(sr_ctx *c, const uint8_t *bytes, size_t nbytes, sr_record *ou
     if (!c || !n_records || (nbytes && !bytes) || nbytes > c->ds.max_batch) return -EINVAL;
     if (max_records && !out) return -EINVAL;
     *n_records = 0;
-    if (nbytes == 0) return 0;
+    if (nbytes == 0) {
+        if (c->ds.nwords) memset(c->h_probed, 0, c->ds.nwords * sizeof(uint64_t));
+        return 0;
+    }
     if (bytes[nbytes - 1] != '\n') return -EINVAL;
+    // every shard alive: nothing can be probed dead (the device bitmap is skipped)
+    if (c->ds.nwords) memset(c->h_probed, 0, c->ds.nwords * sizeof(uint64_t));
     (void)hipSetDevice(c->device);
     // device record capacity: never more lines than bytes
     const size_t cap = max_records < nbytes ? max_records : nbytes;
@@ -267,8 +276,14 @@ int sr_route_batch(sr_ctx *c, const uint8_t *bytes, size_t nbytes, sr_record *ou
         c->d_hash_cap = cap;
     }
     if (hipMemcpyAsync(c->d_in, bytes, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return -EIO;
-    int rc = sr_route_device(c, c->d_in, nbytes, c->d_out, cap, hashes ? c->d_hash : nullptr, c->d_count);
+    RouteParams p = c->ds.params();
+    DeviceState::add_batch(p, c->d_in, nbytes, c->d_out, cap, hashes ? c->d_hash : nullptr, c->d_count, c->d_probed);
+    int rc = launch_variant(c->ds, p, c->stream);
     if (rc) return rc;
+    if (c->ds.dead && c->ds.nwords &&
+        hipMemcpyAsync(c->h_probed, c->d_probed, c->ds.nwords * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                       c->stream) != hipSuccess)
+        return -EIO;
     uint64_t n = 0;
     if (hipMemcpyAsync(&n, c->d_count, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
         return -EIO;

@@ -96,3 +96,13 @@ def test_generator_is_deterministic_and_framed(pkg, oracle):
     assert lens == {64, 256, 1024} and n == m.n_lines
     frac_bad = float((pkg.verdicts(recs["route"]) == 2).mean())
     assert 0.07 < frac_bad < 0.13
+
+
+def test_product_library_has_one_route_kernel_instantiation(pkg):
+    """Ablation variants (some write wrong records by design) never ship: the product library holds
+    exactly one route_kernel instantiation, ABL_NONE (tools/ and `make VARIANTS=1` builds only)."""
+    out = subprocess.run(["nm", "-C", pkg.ROUTE_LIB], capture_output=True, text=True).stdout
+    kernels = {l.split(" ", 2)[-1] for l in out.splitlines()
+               if "route_kernel<" in l and "__device_stub__" not in l}
+    assert kernels == {"void srk::route_kernel<256, 0u>(srk::RouteParams)"}, kernels
+    assert b"SR_VARIANT" not in open(pkg.ROUTE_LIB, "rb").read()
