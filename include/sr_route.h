@@ -155,6 +155,58 @@ int sr_pack_by_owner(sr_ctx *ctx, const uint8_t *d_bytes, size_t nbytes, const s
                      uint8_t *d_out_bytes, size_t out_cap, sr_record *d_out_recs,
                      uint64_t *d_owner_counts);
 
+/* ---- per-downstream MTU packing ------------------------------------------ */
+/* push_to_downstream (sr-main.c:73-83) appends each routed line to its downstream's active buffer,
+ * flushing the buffer first when the line would not fit in DOWNSTREAM_BUF_SIZE (1450) bytes
+ * (ds_schedule_flush, sr-main.c:49-71): per downstream a greedy packing of its lines in arrival
+ * order, starting from the bytes already pending. sr_pack_packets computes it on the device.
+ *
+ * Records are first regrouped stably ("sorted"): the valid lines of downstream 0, 1, ..., N-1 in
+ * arrival order, then every unrouted line (invalid length / format, all dead) in input order.
+ * A packet is a run of consecutive sorted lines, led by `carry` bytes of the downstream's buffer
+ * pending before the batch (only a downstream's first packet of the batch can have carry > 0).
+ * Per downstream with lines in the batch: every packet the batch flushes (open = 0), in order,
+ * then its new pending buffer (open = 1, last). Downstreams without lines get no descriptor; their
+ * pending bytes carry over unchanged, except those probed dead, which are dropped (sr-main.c:106). */
+typedef struct sr_packet {
+    uint32_t first;   /* index in the sorted records of the packet's first line of this batch */
+    uint16_t nlines;  /* lines of this batch in the packet                                   */
+    uint16_t shard;   /* downstream                                                          */
+    uint16_t length;  /* bytes of those lines                                                */
+    uint16_t carry;   /* pending bytes from before the batch that lead the packet            */
+    uint32_t open;    /* 1: the downstream's pending buffer after the batch (not flushed)    */
+} sr_packet;
+
+#define SR_MAX_PACK_DOWNSTREAMS 4096u
+/* Descriptor room that always suffices (two consecutive flushed packets hold > 1450 bytes). */
+#define SR_MAX_PACKETS(nbytes, n_downstreams) \
+    (2u * (uint64_t)(nbytes) / SR_DOWNSTREAM_BUF_SIZE + 5u * (uint64_t)(n_downstreams) + 4u)
+
+/* Device-resident packing of a routed batch (asynchronous on the context's stream):
+ *   d_recs, d_n_records, max_records: the output of sr_route_device(_many) for the batch;
+ *   d_fill_in  : NULL (nothing pending) or n_downstreams u16, pending bytes per downstream (<= 1450);
+ *   d_probed_dead: NULL or the batch's probed-dead bitmap (sr_batch.d_probed_dead);
+ *   d_sorted   : max_records records; d_packets: max_packets descriptors;
+ *   d_counts   : 3 u64 = {descriptors, valid lines, lines} (descriptors past max_packets are not
+ *                written: check d_counts[0] <= max_packets);
+ *   d_fill_out : n_downstreams u16, pending bytes after the batch (may alias d_fill_in only if the
+ *                caller does not need d_fill_in afterwards).
+ * n_downstreams <= SR_MAX_PACK_DOWNSTREAMS. The first call (or one with a larger max_records)
+ * allocates scratch: not inside stream capture. Returns 0, -EINVAL, -ENOMEM, -EIO. */
+int sr_pack_packets(sr_ctx *ctx, const sr_record *d_recs, const uint64_t *d_n_records, size_t max_records,
+                    const uint16_t *d_fill_in, const uint64_t *d_probed_dead, sr_record *d_sorted,
+                    sr_packet *d_packets, size_t max_packets, uint64_t *d_counts, uint16_t *d_fill_out);
+
+/* Host-memory batch, routed and packed in one call (what a data thread's read callback needs):
+ * `fill` (n_downstreams u16) is the pending bytes per downstream before the batch and receives the
+ * pending bytes after it; `sorted` (max_records) the regrouped records; `packets` (max_packets) the
+ * descriptors; probed_dead (ceil(n/64) words, may be NULL) the dead downstreams whose pending
+ * buffer the batch drops. Synchronous. Returns 0, -ENOSPC (records or descriptors did not fit:
+ * outputs incomplete), -EINVAL, -ENOMEM, -EIO. */
+int sr_route_pack_batch(sr_ctx *ctx, const uint8_t *bytes, size_t nbytes, uint16_t *fill, sr_record *sorted,
+                        size_t max_records, size_t *n_records, size_t *n_valid, sr_packet *packets,
+                        size_t max_packets, size_t *n_packets, uint64_t *probed_dead);
+
 /* Wait for all work enqueued by this context. */
 int sr_sync(sr_ctx *ctx);
 

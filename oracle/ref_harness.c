@@ -10,7 +10,12 @@
  * --wrap (nothing is printed): the TRACE/WARN events of sr-main.c:91,102,115,142,184 give, in
  * line order, the verdict, the 64-bit hash, the length and the chosen downstream of every line.
  *
- * Usage: sr_ref_harness <n_downstreams> <alive words hex, comma separated> <in> <out>
+ * With a 5th argument the dead-downstream side effect is recorded too: before the first datagram
+ * every dead downstream gets active_buffer_length = 1 (a pending byte); find_downstream zeroes it
+ * when its probe visits that downstream (sr-main.c:106), and dead downstreams receive no line. The
+ * file receives ceil(N/64) u64 words: bit k = dead downstream k was probed.
+ *
+ * Usage: sr_ref_harness <n_downstreams> <alive words hex, comma separated> <in> <out> [probed]
  *   in : repeated [u32 length][bytes] datagrams (raw, unframed: the reference frames them)
  *   out: one 16-byte event per line: u8 verdict, u8 0, u16 route, i32 length (-1 = not logged),
  *        u64 hash (0 when the reference computed none)
@@ -74,8 +79,8 @@ void __wrap_log_msg(int level, char *format, ...) {
 }
 
 int main(int argc, char **argv) {
-    if (argc != 5) {
-        fprintf(stderr, "usage: %s n_downstreams alive_hex_words in out\n", argv[0]);
+    if (argc != 5 && argc != 6) {
+        fprintf(stderr, "usage: %s n_downstreams alive_hex_words in out [probed]\n", argv[0]);
         return 2;
     }
     int n = atoi(argv[1]);
@@ -96,6 +101,7 @@ int main(int argc, char **argv) {
         ds[i].socket_out = &out_fd;
         hc[i].id = i;
         hc[i].alive = (alive[i / 64] >> (i % 64)) & 1u;
+        if (!hc[i].alive) ds[i].active_buffer_length = 1; /* a pending byte the probe may drop */
     }
     int sv[2];
     if (socketpair(AF_UNIX, SOCK_DGRAM, 0, sv) != 0) return 4;
@@ -122,5 +128,13 @@ int main(int argc, char **argv) {
     if (!out) return 8;
     if (ev_n && fwrite(ev_buf, sizeof(ref_event), ev_n, out) != ev_n) return 9;
     fclose(out);
+    if (argc == 6) {
+        uint64_t *probed = calloc((size_t)(nw ? nw : 1), sizeof(uint64_t));
+        for (int i = 0; i < n; i++)
+            if (!hc[i].alive && ds[i].active_buffer_length == 0) probed[i / 64] |= 1ull << (i % 64);
+        FILE *pf = fopen(argv[5], "wb");
+        if (!pf || (nw && fwrite(probed, 8, (size_t)nw, pf) != (size_t)nw)) return 10;
+        fclose(pf);
+    }
     return 0;
 }

@@ -70,6 +70,97 @@ int sro_find_downstream(uint64_t hash, uint32_t downstream_num, const uint64_t *
     return -1; /* :115-116 */
 }
 
+/* find_downstream with its dead-downstream side effect recorded: every dead downstream k the
+ * probe visits gets active_buffer_length = 0 in the reference (sr-main.c:106); bit k of probed. */
+static int find_downstream_probed(uint64_t hash, uint32_t downstream_num, const uint64_t *alive,
+                                  uint64_t *probed) {
+    if (downstream_num == 0) return -1;
+    int ds_index[downstream_num];
+    for (uint32_t i = 0; i < downstream_num; i++) ds_index[i] = (int)i;
+    for (uint32_t i = downstream_num; i > 0; i--) {
+        uint32_t j = (uint32_t)(hash % i);
+        int k = ds_index[j];
+        if (alive_bit(alive, (uint32_t)k)) return k;
+        probed[k >> 6] |= 1ull << (k & 63); /* :106 */
+        if (j != i - 1) {
+            ds_index[j] = ds_index[i - 1];
+            ds_index[i - 1] = k;
+        }
+        hash = (hash * 7 + 5) / 3;
+    }
+    return -1;
+}
+
+/* The batch's probed-dead bitmap (ceil(n/64) words, zeroed here): the dead downstreams whose
+ * pending buffer the reference drops while routing the batch (sr-main.c:106). */
+void sro_probed_dead(const uint8_t *buf, size_t nbytes, uint32_t downstream_num,
+                     const uint64_t *alive, uint64_t *probed) {
+    memset(probed, 0, ((downstream_num + 63) / 64) * sizeof(uint64_t));
+    const uint8_t *ptr = buf, *delim;
+    size_t rem = nbytes;
+    while (rem > 0 && (delim = memchr(ptr, '\n', rem)) != NULL) {
+        size_t len = (size_t)(delim + 1 - ptr);
+        uint64_t h;
+        if (len > 5 && len < SR_DOWNSTREAM_BUF_SIZE && sro_hash(ptr, len, &h) == 0)
+            (void)find_downstream_probed(h, downstream_num, alive, probed);
+        ptr = delim + 1;
+        rem -= len;
+    }
+}
+
+/* push_to_downstream (sr-main.c:73-83) + the flush it triggers (ds_schedule_flush, :49-71) over a
+ * routed batch, in the descriptor form of sr_pack_packets (include/sr_route.h): per downstream, in
+ * arrival order, a line that would overflow the DOWNSTREAM_BUF_SIZE buffer first flushes it.
+ * Returns 0, or -1 if max_packets is too small. */
+int sro_pack_packets(const sr_record *recs, size_t n, uint32_t nds, const uint16_t *fill_in,
+                     const uint64_t *probed_dead, sr_record *sorted, sr_packet *packets,
+                     size_t max_packets, size_t *n_packets, size_t *n_valid, uint16_t *fill_out) {
+    size_t *start = calloc((size_t)nds + 2, sizeof(size_t));
+    if (!start) return -1;
+    for (size_t i = 0; i < n; i++) start[(recs[i].route < nds ? recs[i].route : nds) + 1]++;
+    for (uint32_t k = 0; k <= nds; k++) start[k + 1] += start[k];
+    size_t *pos = calloc((size_t)nds + 1, sizeof(size_t));
+    if (!pos) return -1;
+    memcpy(pos, start, ((size_t)nds + 1) * sizeof(size_t));
+    for (size_t i = 0; i < n; i++) sorted[pos[recs[i].route < nds ? recs[i].route : nds]++] = recs[i];
+    size_t np = 0;
+    int rc = 0;
+    for (uint32_t s = 0; s < nds; s++) {
+        unsigned fill = fill_in ? fill_in[s] : 0;
+        size_t pstart = start[s];
+        unsigned pcarry = fill, plen = 0;
+        for (size_t q = start[s]; q < start[s + 1]; q++) {
+            unsigned L = sorted[q].length;
+            if (fill + L > SR_DOWNSTREAM_BUF_SIZE) { /* sr-main.c:75-78 */
+                if (np < max_packets)
+                    packets[np] = (sr_packet){(uint32_t)pstart, (uint16_t)(q - pstart), (uint16_t)s,
+                                              (uint16_t)plen, (uint16_t)pcarry, 0};
+                np++;
+                fill = 0; /* ds_schedule_flush: a new active buffer, sr-main.c:63-65 */
+                pstart = q;
+                pcarry = 0;
+                plen = 0;
+            }
+            fill += L; /* :80-82 */
+            plen += L;
+        }
+        if (start[s + 1] > start[s]) {
+            if (np < max_packets)
+                packets[np] = (sr_packet){(uint32_t)pstart, (uint16_t)(start[s + 1] - pstart), (uint16_t)s,
+                                          (uint16_t)plen, (uint16_t)pcarry, 1};
+            np++;
+        }
+        if (probed_dead && ((probed_dead[s >> 6] >> (s & 63)) & 1u)) fill = 0; /* sr-main.c:106 */
+        fill_out[s] = (uint16_t)fill;
+    }
+    if (np > max_packets) rc = -1;
+    *n_packets = np;
+    *n_valid = start[nds];
+    free(start);
+    free(pos);
+    return rc;
+}
+
 /* sr-main.c:175-189 over a batch of framed datagrams laid back to back. Every framed datagram
  * ends in '\n', so the lines of the concatenation are exactly the lines of the datagrams and
  * datagram boundaries need not be known. Bytes after the last '\n' are not a line. */

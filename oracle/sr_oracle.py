@@ -19,8 +19,12 @@ import numpy as np
 ORACLE_DIR = os.path.dirname(os.path.abspath(__file__))
 ORACLE_LIB = os.path.join(ORACLE_DIR, "_build", "libsr_oracle.so")
 REF_HARNESS = os.path.join(ORACLE_DIR, "_ref", "sr_ref_harness")
+REF_ROUTER = os.path.join(ORACLE_DIR, "_ref", "sr_ref_router")
+REF_TEST_HOSTNAME = "sr-test-host"   # what ref_router_harness.c makes gethostname() return
 
 RECORD_DTYPE = np.dtype([("offset", "<u4"), ("length", "<u2"), ("route", "<u2")])
+PACKET_DTYPE = np.dtype([("first", "<u4"), ("nlines", "<u2"), ("shard", "<u2"), ("length", "<u2"),
+                         ("carry", "<u2"), ("open", "<u4")])
 REF_EVENT_DTYPE = np.dtype([("verdict", "u1"), ("zero", "u1"), ("route", "<u2"), ("length", "<i4"),
                             ("hash", "<u8")])
 
@@ -40,6 +44,11 @@ def lib() -> ctypes.CDLL:
         L.sro_find_downstream.argtypes = [ctypes.c_uint64, ctypes.c_uint32, vp]
         L.sro_route_batch.restype = sz
         L.sro_route_batch.argtypes = [vp, sz, ctypes.c_uint32, vp, vp, sz, vp]
+        L.sro_probed_dead.restype = None
+        L.sro_probed_dead.argtypes = [vp, sz, ctypes.c_uint32, vp, vp]
+        L.sro_pack_packets.restype = ctypes.c_int
+        L.sro_pack_packets.argtypes = [vp, sz, ctypes.c_uint32, vp, vp, vp, vp, sz, ctypes.POINTER(sz),
+                                       ctypes.POINTER(sz), vp]
         L.sro_bench.restype = ctypes.c_int
         L.sro_bench.argtypes = [vp, vp, sz, ctypes.c_uint32, vp, ctypes.c_int, ctypes.c_double,
                                 ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
@@ -89,6 +98,65 @@ def route(data, n_downstreams: int, alive=None, max_records: int | None = None):
     return out[:k], hs[:k], n
 
 
+def probed_dead(data, n_downstreams: int, alive) -> np.ndarray:
+    """Shard ids of the dead downstreams the batch's probes visit (sr-main.c:106)."""
+    buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else np.ascontiguousarray(data, dtype=np.uint8)
+    w = alive_words(n_downstreams, alive)
+    out = np.zeros(max((n_downstreams + 63) // 64, 1), dtype=np.uint64)
+    lib().sro_probed_dead(buf.ctypes.data, buf.size, n_downstreams, w.ctypes.data, out.ctypes.data)
+    bits = np.unpackbits(out.view(np.uint8), bitorder="little")[:n_downstreams]
+    return np.nonzero(bits)[0]
+
+
+def pack_packets(recs: np.ndarray, n_downstreams: int, fill_in=None, probed=()):
+    """push_to_downstream + ds_schedule_flush (sr-main.c:49-83) over routed records, in the form of
+    sr_pack_packets. Returns (sorted records, packets (PACKET_DTYPE), fill_out u16[N], n_valid)."""
+    recs = np.ascontiguousarray(recs, dtype=RECORD_DTYPE)
+    n = len(recs)
+    fin = np.zeros(max(n_downstreams, 1), dtype=np.uint16)
+    if fill_in is not None:
+        fin[:n_downstreams] = np.asarray(fill_in, dtype=np.uint16)
+    pw = np.zeros(max((n_downstreams + 63) // 64, 1), dtype=np.uint64)
+    for k in probed:
+        pw[int(k) >> 6] |= np.uint64(1) << np.uint64(int(k) & 63)
+    sorted_ = np.zeros(max(n, 1), dtype=RECORD_DTYPE)
+    cap = 2 * n + 5 * n_downstreams + 4
+    pk = np.zeros(cap, dtype=PACKET_DTYPE)
+    fout = np.zeros(max(n_downstreams, 1), dtype=np.uint16)
+    npk, nv = ctypes.c_size_t(), ctypes.c_size_t()
+    rc = lib().sro_pack_packets(recs.ctypes.data, n, n_downstreams, fin.ctypes.data, pw.ctypes.data,
+                                sorted_.ctypes.data, pk.ctypes.data, cap, ctypes.byref(npk), ctypes.byref(nv),
+                                fout.ctypes.data)
+    if rc:
+        raise RuntimeError("sro_pack_packets: descriptor room")
+    return sorted_[:n], pk[: npk.value], fout[:n_downstreams], nv.value
+
+
+def materialize(data, sorted_recs: np.ndarray, packets: np.ndarray, pending: dict, fill_out=None):
+    """Packet bytes from descriptors: {shard: [flushed packet bytes, ...]} and the new pending
+    buffers {shard: bytes}. pending: {shard: bytes pending before the batch}; fill_out (optional):
+    the pending lengths after the batch (a shard without descriptors whose fill_out is 0 was
+    probed dead: its pending bytes are dropped, sr-main.c:106)."""
+    raw = bytes(data)
+    out, new_pending = {}, dict(pending)
+    if fill_out is not None:
+        for s, f in enumerate(fill_out):
+            if int(f) == 0:
+                new_pending[s] = b""
+    for p in packets:
+        s = int(p["shard"])
+        body = b"".join(raw[int(r["offset"]): int(r["offset"]) + int(r["length"])]
+                        for r in sorted_recs[int(p["first"]): int(p["first"]) + int(p["nlines"])])
+        assert len(body) == int(p["length"])
+        lead = pending.get(s, b"")[: int(p["carry"])]
+        assert len(lead) == int(p["carry"])
+        if int(p["open"]):
+            new_pending[s] = lead + body
+        else:
+            out.setdefault(s, []).append(lead + body)
+    return out, new_pending
+
+
 def bench(batches: Sequence[np.ndarray], n_downstreams: int, alive, threads: int, seconds: float):
     """Time the restatement (the reference's serial per-line loop) on host cores.
     Returns (lines, bytes, wall_seconds)."""
@@ -108,19 +176,89 @@ def have_reference() -> bool:
     return os.path.exists(REF_HARNESS)
 
 
-def run_reference(dgrams: Sequence[bytes], n_downstreams: int, alive=None) -> np.ndarray:
+def run_reference(dgrams: Sequence[bytes], n_downstreams: int, alive=None, probed: bool = False):
     """Feed raw datagrams through the REFERENCE's udp_read_cb (compiled from /root/reference) and
-    return its per-line events (REF_EVENT_DTYPE)."""
+    return its per-line events (REF_EVENT_DTYPE); with probed=True also the shard ids of the dead
+    downstreams whose pending buffer the reference dropped (sr-main.c:106)."""
     w = alive_words(n_downstreams, alive)
     with tempfile.TemporaryDirectory() as td:
-        fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
+        fin, fout, fpr = os.path.join(td, "in.bin"), os.path.join(td, "out.bin"), os.path.join(td, "pr.bin")
         with open(fin, "wb") as f:
             for d in dgrams:
                 f.write(struct.pack("<I", len(d)))
                 f.write(d)
         hexw = ",".join(f"{int(x):x}" for x in w)
-        subprocess.run([REF_HARNESS, str(n_downstreams), hexw, fin, fout], check=True)
-        return np.fromfile(fout, dtype=REF_EVENT_DTYPE)
+        subprocess.run([REF_HARNESS, str(n_downstreams), hexw, fin, fout] + ([fpr] if probed else []), check=True)
+        ev = np.fromfile(fout, dtype=REF_EVENT_DTYPE)
+        if not probed:
+            return ev
+        pw = np.fromfile(fpr, dtype=np.uint64)
+        bits = np.unpackbits(pw.view(np.uint8), bitorder="little")[:n_downstreams] if pw.size else np.zeros(0)
+        return ev, np.nonzero(bits)[0]
+
+
+# ---- one reference data thread driven by scripted events (oracle/ref_router_harness.c) ---------
+EV_ALIVE, EV_FLUSH, EV_PING = 0xFFFFFFF1, 0xFFFFFFF2, 0xFFFFFFF3
+
+
+def write_events(path: str, events, n_downstreams: int) -> None:
+    """events: ("dgram", bytes) | ("alive", [0/1 per downstream]) | ("flush",) | ("ping",)."""
+    with open(path, "wb") as f:
+        for e in events:
+            if e[0] == "dgram":
+                f.write(struct.pack("<I", len(e[1])))
+                f.write(e[1])
+            elif e[0] == "alive":
+                f.write(struct.pack("<I", EV_ALIVE))
+                f.write(alive_words(n_downstreams, e[1]).tobytes())
+            elif e[0] == "flush":
+                f.write(struct.pack("<I", EV_FLUSH))
+            elif e[0] == "ping":
+                f.write(struct.pack("<I", EV_PING))
+            else:
+                raise ValueError(e)
+
+
+def parse_router_output(blob: bytes):
+    """-> {"packets": {ds: [bytes]}, "logs": [(level, text bytes)], "final": {ds: (pending, traffic, packets)}}"""
+    res = {"packets": {}, "logs": [], "final": {}}
+    i = 0
+    while i < len(blob):
+        t = blob[i]
+        if t == 1:
+            d, l = struct.unpack_from("<HH", blob, i + 1)
+            res["packets"].setdefault(d, []).append(blob[i + 5: i + 5 + l])
+            i += 5 + l
+        elif t == 2:
+            lv, l = struct.unpack_from("<BH", blob, i + 1)
+            res["logs"].append((lv, blob[i + 4: i + 4 + l]))
+            i += 4 + l
+        elif t == 3:
+            d, l = struct.unpack_from("<HH", blob, i + 1)
+            pend = blob[i + 5: i + 5 + l]
+            tr, pk = struct.unpack_from("<II", blob, i + 5 + l)
+            res["final"][d] = (pend, tr, pk)
+            i += 13 + l
+        else:
+            raise ValueError(f"bad event type {t} at {i}")
+    return res
+
+
+def have_reference_router() -> bool:
+    return os.path.exists(REF_ROUTER)
+
+
+def run_reference_router(config_text: str, events, n_downstreams: int):
+    """Run the REFERENCE data thread (init_config + udp_read_cb + ds_flush_timer_cb + ping_cb +
+    ds_flush_cb, compiled from /root/reference) over scripted events."""
+    with tempfile.TemporaryDirectory() as td:
+        cfg, fin, fout = (os.path.join(td, x) for x in ("sr.conf", "in.bin", "out.bin"))
+        with open(cfg, "w") as f:
+            f.write(config_text)
+        write_events(fin, events, n_downstreams)
+        subprocess.run([REF_ROUTER, cfg, fin, fout], check=True)
+        with open(fout, "rb") as f:
+            return parse_router_output(f.read())
 
 
 def pack_by_owner(data, recs: np.ndarray, n_owners: int):

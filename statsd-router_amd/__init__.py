@@ -46,8 +46,8 @@ assert RECORD_DTYPE.itemsize == 8
 # every function the header declares (tests check the library exports exactly these)
 ABI_FUNCTIONS = (
     "sr_frame_datagram", "sr_frame_datagrams", "sr_open", "sr_set_alive", "sr_set_stream",
-    "sr_route_batch", "sr_route_device", "sr_route_device_many", "sr_pack_by_owner", "sr_sync", "sr_close",
-    "sr_version",
+    "sr_route_batch", "sr_last_probed_dead", "sr_route_device", "sr_route_device_many", "sr_pack_by_owner",
+    "sr_sync", "sr_close", "sr_version",
 )
 SR_MAX_OWNERS = 64
 
@@ -63,6 +63,7 @@ class SrBatch(ctypes.Structure):
     _fields_ = [
         ("d_bytes", ctypes.c_void_p), ("nbytes", ctypes.c_size_t), ("d_out", ctypes.c_void_p),
         ("max_records", ctypes.c_size_t), ("d_hashes", ctypes.c_void_p), ("d_n_records", ctypes.c_void_p),
+        ("d_probed_dead", ctypes.c_void_p),
     ]
 
 
@@ -109,6 +110,7 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_set_alive": (ctypes.c_int, [vp, u64p]),
         "sr_set_stream": (ctypes.c_int, [vp, vp]),
         "sr_route_batch": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, c_size_p, vp]),
+        "sr_last_probed_dead": (ctypes.c_int, [vp, u64p]),
         "sr_route_device": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp, vp]),
         "sr_route_device_many": (ctypes.c_int, [vp, ctypes.POINTER(SrBatch), ctypes.c_size_t]),
         "sr_pack_by_owner": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, ctypes.c_uint32,
@@ -190,6 +192,13 @@ def gen_stream(nbytes: int, line_lens: Iterable[int], seed: int, p_invalid: floa
     return Stream(out[:n], dl[: min(nd.value, dcap)].copy(), nl.value)
 
 
+def bitmap_shards(words, n: int) -> np.ndarray:
+    """Shard ids whose bit is set in a ceil(n/64)-word bitmap."""
+    w = np.asarray(words, dtype=np.uint64)
+    bits = np.unpackbits(w.view(np.uint8), bitorder="little")[:n]
+    return np.nonzero(bits)[0]
+
+
 # ---- the router context -------------------------------------------------------------------------
 def alive_words(n_downstreams: int, alive: Iterable[int] | np.ndarray | None) -> np.ndarray:
     """Bitmap words from a 0/1 sequence (None = all alive)."""
@@ -263,6 +272,15 @@ class Router:
         k = min(n.value, cap)
         return out[:k], (hashes[:k] if want_hashes else None), n.value
 
+    def last_probed_dead(self) -> np.ndarray:
+        """sr_last_probed_dead: the dead downstreams probed by the last route() (sr-main.c:106) as
+        a sorted array of shard ids."""
+        nw = max((self.n_downstreams + 63) // 64, 1)
+        w = np.zeros(nw, dtype=np.uint64)
+        _check(self._lib.sr_last_probed_dead(self._h, w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))),
+               "sr_last_probed_dead")
+        return bitmap_shards(w, self.n_downstreams)
+
     def route_device(self, d_bytes: int, nbytes: int, d_out: int, max_records: int,
                      d_hashes: int | None, d_count: int) -> None:
         """sr_route_device with raw device pointers (e.g. torch tensors' data_ptr())."""
@@ -271,10 +289,13 @@ class Router:
                "sr_route_device")
 
     def route_device_many(self, batches) -> None:
-        """sr_route_device_many: batches = [(d_bytes, nbytes, d_out, max_records, d_hashes, d_count), ...]."""
+        """sr_route_device_many: batches = [(d_bytes, nbytes, d_out, max_records, d_hashes, d_count
+        [, d_probed_dead]), ...]."""
         arr = (SrBatch * max(len(batches), 1))()
-        for i, (db, nb, do, mr, dh, dc) in enumerate(batches):
-            arr[i] = SrBatch(db, nb, do, mr, dh or None, dc)
+        for i, b in enumerate(batches):
+            db, nb, do, mr, dh, dc = b[:6]
+            dp = b[6] if len(b) > 6 else None
+            arr[i] = SrBatch(db, nb, do, mr, dh or None, dc, dp or None)
         _check(self._lib.sr_route_device_many(self._h, arr, len(batches)), "sr_route_device_many")
 
     def pack_by_owner(self, d_bytes: int, nbytes: int, d_recs: int, d_n_records: int, max_records: int,

@@ -15,6 +15,7 @@
 #include <new>
 
 #include "../../include/sr_route.h"
+#include "mtu_kernel.hpp"
 #include "regroup_kernel.hpp"
 #include "route_host.hpp"
 
@@ -38,7 +39,20 @@ struct sr_ctx {
     uint2 *d_pack_tiles;          // tile counts | tile bases
     size_t pack_tiles_cap;        // entries per array
     uint64_t *d_owner_start;
+    // scratch of sr_pack_packets (capacities: record tiles, chunks)
+    uint32_t mtu_ntiles, mtu_chunks;
+    uint32_t *d_mtu_tiles, *d_mtu_keys, *d_mtu_chunks;
+    uint64_t *d_mtu_table;
+    // buffers of sr_route_pack_batch
+    sr_record *d_sorted;
+    size_t d_sorted_cap;
+    sr_packet *d_packets;
+    size_t d_packets_cap;
+    uint16_t *d_fill;             // [2][nds]: in, out
+    uint64_t *d_mcounts;          // 3 u64
 };
+
+static void free_ptr(void *p) { (void)hipFree(p); }
 
 // The product launches exactly one instantiation, ABL_NONE. Ablation variants (records wrong by
 // design in some of them) exist only in builds made with -DSR_ABLATION_VARIANTS (`make VARIANTS=1`,
@@ -111,6 +125,14 @@ void sr_close(sr_ctx *c) {
     free(c->h_probed);
     (void)hipFree(c->d_pack_tiles);
     (void)hipFree(c->d_owner_start);
+    free_ptr(c->d_mtu_tiles);
+    free_ptr(c->d_mtu_keys);
+    free_ptr(c->d_mtu_chunks);
+    free_ptr(c->d_mtu_table);
+    free_ptr(c->d_sorted);
+    free_ptr(c->d_packets);
+    free_ptr(c->d_fill);
+    free_ptr(c->d_mcounts);
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     free(c);
 }
@@ -244,6 +266,148 @@ int sr_pack_by_owner(sr_ctx *c, const uint8_t *d_bytes, size_t nbytes, const sr_
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
     return 0;
+}
+
+// Scratch of the packing kernels for max_records records (grown, never shrunk; not in capture).
+static int mtu_reserve(sr_ctx *c, size_t max_records) {
+    const uint32_t nds = c->ds.nds;
+    const uint32_t ntiles = (uint32_t)((max_records + kMtuTile - 1) / kMtuTile) + 1;
+    const uint32_t chunks = (uint32_t)((max_records + kMtuChunk - 1) / kMtuChunk) + nds + 1;
+    if (ntiles > c->mtu_ntiles) {
+        free_ptr(c->d_mtu_tiles);
+        c->d_mtu_tiles = nullptr;
+        c->mtu_ntiles = 0;
+        if (hipMalloc(&c->d_mtu_tiles, (size_t)(nds + 1) * ntiles * sizeof(uint32_t)) != hipSuccess) return -ENOMEM;
+        c->mtu_ntiles = ntiles;
+    }
+    if (!c->d_mtu_keys && hipMalloc(&c->d_mtu_keys, (2 * (size_t)nds + 4) * sizeof(uint32_t)) != hipSuccess)
+        return -ENOMEM;
+    if (chunks > c->mtu_chunks) {
+        free_ptr(c->d_mtu_chunks);
+        free_ptr(c->d_mtu_table);
+        c->d_mtu_chunks = nullptr;
+        c->d_mtu_table = nullptr;
+        c->mtu_chunks = 0;
+        // shard, entry (+ nds scratch), open, first descriptor per chunk
+        if (hipMalloc(&c->d_mtu_chunks, (4 * (size_t)chunks + nds) * sizeof(uint32_t)) != hipSuccess) return -ENOMEM;
+        if (hipMalloc(&c->d_mtu_table, (size_t)chunks * kMtuX * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+        c->mtu_chunks = chunks;
+    }
+    return 0;
+}
+
+int sr_pack_packets(sr_ctx *c, const sr_record *d_recs, const uint64_t *d_n_records, size_t max_records,
+                    const uint16_t *d_fill_in, const uint64_t *d_probed_dead, sr_record *d_sorted,
+                    sr_packet *d_packets, size_t max_packets, uint64_t *d_counts, uint16_t *d_fill_out) {
+    if (!c || !d_n_records || !d_counts || (c->ds.nds && !d_fill_out)) return -EINVAL;
+    if (c->ds.nds > SR_MAX_PACK_DOWNSTREAMS || max_records > 0xFFFFFFF0ull) return -EINVAL;
+    if (max_records && (!d_recs || !d_sorted)) return -EINVAL;
+    if (max_packets && !d_packets) return -EINVAL;
+    (void)hipSetDevice(c->device);
+    int rc = mtu_reserve(c, max_records);
+    if (rc) return rc;
+    const uint32_t nds = c->ds.nds;
+    MtuParams p;
+    memset(&p, 0, sizeof(p));
+    p.recs = d_recs;
+    p.n_records = d_n_records;
+    p.max_records = (uint32_t)max_records;
+    p.nds = nds;
+    p.ntiles = (uint32_t)((max_records + kMtuTile - 1) / kMtuTile);
+    if (p.ntiles == 0) p.ntiles = 1;
+    p.max_chunks = (uint32_t)((max_records + kMtuChunk - 1) / kMtuChunk) + nds;
+    p.fill_in = d_fill_in;
+    p.probed_dead = d_probed_dead;
+    p.tile_counts = c->d_mtu_tiles;
+    p.key_start = c->d_mtu_keys;
+    p.chunk_first = c->d_mtu_keys + nds + 2;
+    p.chunk_shard = c->d_mtu_chunks;
+    p.chunk_entry = c->d_mtu_chunks + p.max_chunks;           // + nds scratch words after the chunk rows
+    p.chunk_open = p.chunk_entry + p.max_chunks + nds;
+    p.chunk_pk = p.chunk_open + p.max_chunks;
+    p.table = c->d_mtu_table;
+    p.sorted = d_sorted;
+    p.packets = d_packets;
+    p.max_packets = max_packets;
+    p.counts = d_counts;
+    p.fill_out = d_fill_out;
+    hipLaunchKernelGGL(mtu_count_kernel, dim3(p.ntiles), dim3(64), 0, c->stream, p);
+    hipLaunchKernelGGL(mtu_scan_kernel, dim3(1), dim3(1024), 0, c->stream, p);
+    hipLaunchKernelGGL(mtu_scatter_kernel, dim3(p.ntiles), dim3(64), 0, c->stream, p);
+    if (p.max_chunks) hipLaunchKernelGGL(mtu_table_kernel, dim3(p.max_chunks), dim3(kMtuBlock), 0, c->stream, p);
+    hipLaunchKernelGGL(mtu_chain_kernel, dim3(1), dim3(1024), 0, c->stream, p);
+    if (p.max_chunks) hipLaunchKernelGGL(mtu_emit_kernel, dim3(p.max_chunks), dim3(kMtuBlock), 0, c->stream, p);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+static int grow(void **ptr, size_t *cap, size_t need, size_t elem) {
+    if (need <= *cap) return 0;
+    free_ptr(*ptr);
+    *ptr = nullptr;
+    *cap = 0;
+    if (hipMalloc(ptr, (need ? need : 1) * elem) != hipSuccess) return -ENOMEM;
+    *cap = need;
+    return 0;
+}
+
+int sr_route_pack_batch(sr_ctx *c, const uint8_t *bytes, size_t nbytes, uint16_t *fill, sr_record *sorted,
+                        size_t max_records, size_t *n_records, size_t *n_valid, sr_packet *packets,
+                        size_t max_packets, size_t *n_packets, uint64_t *probed_dead) {
+    if (!c || !n_records || !n_valid || !n_packets || (nbytes && !bytes) || nbytes > c->ds.max_batch) return -EINVAL;
+    if ((c->ds.nds && !fill) || (max_records && !sorted) || (max_packets && !packets)) return -EINVAL;
+    if (c->ds.nds > SR_MAX_PACK_DOWNSTREAMS) return -EINVAL;
+    *n_records = *n_valid = *n_packets = 0;
+    const uint32_t nw = c->ds.nwords;
+    if (nbytes == 0) {
+        if (probed_dead && nw) memset(probed_dead, 0, nw * sizeof(uint64_t));
+        return 0;
+    }
+    if (bytes[nbytes - 1] != '\n') return -EINVAL;
+    (void)hipSetDevice(c->device);
+    const size_t cap = nbytes;   // never more lines than bytes
+    const size_t pcap = (size_t)SR_MAX_PACKETS(nbytes, c->ds.nds);
+    int rc;
+    if ((rc = grow((void **)&c->d_out, &c->d_out_cap, cap, sizeof(sr_record)))) return rc;
+    if ((rc = grow((void **)&c->d_sorted, &c->d_sorted_cap, cap, sizeof(sr_record)))) return rc;
+    if ((rc = grow((void **)&c->d_packets, &c->d_packets_cap, pcap, sizeof(sr_packet)))) return rc;
+    if (!c->d_fill && hipMalloc(&c->d_fill, (2 * (size_t)c->ds.nds + 2) * sizeof(uint16_t)) != hipSuccess)
+        return -ENOMEM;
+    if (!c->d_mcounts && hipMalloc(&c->d_mcounts, 4 * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+    const size_t nds = c->ds.nds;
+    if (hipMemcpyAsync(c->d_in, bytes, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return -EIO;
+    if (nds && hipMemcpyAsync(c->d_fill, fill, nds * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return -EIO;
+    RouteParams p = c->ds.params();
+    DeviceState::add_batch(p, c->d_in, nbytes, c->d_out, cap, nullptr, c->d_count, c->d_probed);
+    if ((rc = launch_variant(c->ds, p, c->stream))) return rc;
+    if ((rc = sr_pack_packets(c, c->d_out, c->d_count, cap, c->d_fill, c->ds.dead ? c->d_probed : nullptr,
+                              c->d_sorted, c->d_packets, pcap, c->d_mcounts, c->d_fill + nds)))
+        return rc;
+    uint64_t cnt[3] = {0, 0, 0};
+    if (hipMemcpyAsync(cnt, c->d_mcounts, sizeof(cnt), hipMemcpyDeviceToHost, c->stream) != hipSuccess) return -EIO;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return -EIO;
+    const size_t nr = (size_t)cnt[2], np = (size_t)cnt[0];
+    const size_t cr = nr < max_records ? nr : max_records, cp = np < max_packets ? np : max_packets;
+    if (cr && hipMemcpyAsync(sorted, c->d_sorted, cr * sizeof(sr_record), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        return -EIO;
+    if (cp && hipMemcpyAsync(packets, c->d_packets, cp * sizeof(sr_packet), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        return -EIO;
+    if (nds && hipMemcpyAsync(fill, c->d_fill + nds, nds * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+        return -EIO;
+    if (probed_dead && nw) {
+        if (c->ds.dead) {
+            if (hipMemcpyAsync(probed_dead, c->d_probed, nw * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream) !=
+                hipSuccess)
+                return -EIO;
+        } else {
+            memset(probed_dead, 0, nw * sizeof(uint64_t));
+        }
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return -EIO;
+    *n_records = nr;
+    *n_valid = (size_t)cnt[1];
+    *n_packets = np;
+    return (nr > max_records || np > max_packets) ? -ENOSPC : 0;
 }
 
 int sr_route_batch(sr_ctx *c, const uint8_t *bytes, size_t nbytes, sr_record *out, size_t max_records,
