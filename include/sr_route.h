@@ -207,6 +207,11 @@ int sr_route_pack_batch(sr_ctx *ctx, const uint8_t *bytes, size_t nbytes, uint16
                         size_t max_records, size_t *n_records, size_t *n_valid, sr_packet *packets,
                         size_t max_packets, size_t *n_packets, uint64_t *probed_dead);
 
+/* Page-locked host memory for the batches and outputs of the host-memory calls (their copies then
+ * run at full link rate). NULL on failure. */
+void *sr_alloc_host(size_t bytes);
+void sr_free_host(void *p);
+
 /* Wait for all work enqueued by this context. */
 int sr_sync(sr_ctx *ctx);
 

@@ -47,8 +47,17 @@ assert RECORD_DTYPE.itemsize == 8
 ABI_FUNCTIONS = (
     "sr_frame_datagram", "sr_frame_datagrams", "sr_open", "sr_set_alive", "sr_set_stream",
     "sr_route_batch", "sr_last_probed_dead", "sr_route_device", "sr_route_device_many", "sr_pack_by_owner",
-    "sr_sync", "sr_close", "sr_version",
+    "sr_pack_packets", "sr_route_pack_batch", "sr_alloc_host", "sr_free_host", "sr_sync", "sr_close", "sr_version",
 )
+SR_MAX_PACK_DOWNSTREAMS = 4096
+PACKET_DTYPE = np.dtype([("first", "<u4"), ("nlines", "<u2"), ("shard", "<u2"), ("length", "<u2"),
+                         ("carry", "<u2"), ("open", "<u4")])
+assert PACKET_DTYPE.itemsize == 16
+
+
+def max_packets(nbytes: int, n_downstreams: int) -> int:
+    """SR_MAX_PACKETS: descriptor room that always suffices."""
+    return 2 * nbytes // 1450 + 5 * n_downstreams + 4
 SR_MAX_OWNERS = 64
 
 
@@ -115,6 +124,11 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_route_device_many": (ctypes.c_int, [vp, ctypes.POINTER(SrBatch), ctypes.c_size_t]),
         "sr_pack_by_owner": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, ctypes.c_uint32,
                                             vp, ctypes.c_size_t, vp, vp]),
+        "sr_pack_packets": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp, vp, vp, vp, ctypes.c_size_t, vp, vp]),
+        "sr_route_pack_batch": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, c_size_p, c_size_p,
+                                               vp, ctypes.c_size_t, c_size_p, vp]),
+        "sr_alloc_host": (vp, [ctypes.c_size_t]),
+        "sr_free_host": (None, [vp]),
         "sr_sync": (ctypes.c_int, [vp]),
         "sr_close": (None, [vp]),
         "sr_version": (ctypes.c_char_p, []),
@@ -305,6 +319,35 @@ class Router:
         _check(self._lib.sr_pack_by_owner(self._h, vp(d_bytes), nbytes, vp(d_recs), vp(d_n_records), max_records,
                                           n_owners, vp(d_out_bytes), out_cap, vp(d_out_recs), vp(d_owner_counts)),
                "sr_pack_by_owner")
+
+    def route_pack(self, data, fill=None):
+        """sr_route_pack_batch on host memory: route + per-downstream MTU packing. fill: pending
+        bytes per downstream before the batch (None = 0). Returns (sorted records, packets,
+        fill after, n_valid, probed-dead shard ids)."""
+        buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else np.ascontiguousarray(data, dtype=np.uint8)
+        nbytes, n = int(buf.size), self.n_downstreams
+        f = np.zeros(max(n, 1), dtype=np.uint16)
+        if fill is not None:
+            f[:n] = np.asarray(fill, dtype=np.uint16)
+        srt = np.zeros(max(nbytes, 1), dtype=RECORD_DTYPE)
+        mp = max_packets(nbytes, n)
+        pk = np.zeros(mp, dtype=PACKET_DTYPE)
+        pw = np.zeros(max((n + 63) // 64, 1), dtype=np.uint64)
+        nr, nv, npk = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        _check(self._lib.sr_route_pack_batch(self._h, buf.ctypes.data if nbytes else None, nbytes, f.ctypes.data,
+                                             srt.ctypes.data, srt.size, ctypes.byref(nr), ctypes.byref(nv),
+                                             pk.ctypes.data, mp, ctypes.byref(npk), pw.ctypes.data),
+               "sr_route_pack_batch")
+        return srt[: nr.value], pk[: npk.value], f[:n].copy(), nv.value, bitmap_shards(pw, n)
+
+    def pack_packets(self, d_recs: int, d_n_records: int, max_records: int, d_fill_in: int | None,
+                     d_probed_dead: int | None, d_sorted: int, d_packets: int, max_pk: int, d_counts: int,
+                     d_fill_out: int) -> None:
+        """sr_pack_packets with raw device pointers (asynchronous on the context's stream)."""
+        vp = ctypes.c_void_p
+        _check(self._lib.sr_pack_packets(self._h, vp(d_recs), vp(d_n_records), max_records, vp(d_fill_in or 0),
+                                         vp(d_probed_dead or 0), vp(d_sorted), vp(d_packets), max_pk, vp(d_counts),
+                                         vp(d_fill_out)), "sr_pack_packets")
 
     def sync(self) -> None:
         _check(self._lib.sr_sync(self._h), "sr_sync")

@@ -108,6 +108,15 @@ size_t sr_frame_datagrams(uint8_t *dst, size_t dst_cap, const uint8_t *const *dg
     return pos;
 }
 
+void *sr_alloc_host(size_t bytes) {
+    void *p = nullptr;
+    return hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocDefault) == hipSuccess ? p : nullptr;
+}
+
+void sr_free_host(void *p) {
+    if (p) (void)hipHostFree(p);
+}
+
 const char *sr_version(void) {
     return "statsd-router-mi355x 0.5 (gfx950 route_kernel: 16 KiB tiles x 256 threads, per-batch scanners, up to 32 batches per launch)";
 }

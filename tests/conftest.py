@@ -71,3 +71,33 @@ def torch_stream():
     finally:
         torch.cuda.synchronize()
         torch.cuda.set_stream(prev)
+
+
+def router_fixtures():
+    return sorted(os.path.basename(p)[:-5] for p in glob.glob(os.path.join(GOLDEN, "router_*.json")))
+
+
+def load_router_fixture(name):
+    """A scripted data-thread session and what the compiled reference did with it
+    (tests/golden/make_router_golden.py)."""
+    import base64
+
+    with open(os.path.join(GOLDEN, name + ".json")) as f:
+        d = json.load(f)
+    dec = base64.b64decode
+    events = []
+    for e in d["events"]:
+        if e[0] == "dgram":
+            events.append(("dgram", dec(e[1])))
+        elif e[0] == "alive":
+            events.append(("alive", e[1]))
+        else:
+            events.append((e[0],))
+    return {
+        "n": d["n_downstreams"], "ds_hosts": d["ds_hosts"], "ds_data_ports": d["ds_data_ports"],
+        "ping_prefix": d["ping_prefix"], "hostname": d["hostname"], "data_port": d["data_port"],
+        "events": events,
+        "packets": {int(k): [dec(p) for p in v] for k, v in d["packets"].items()},
+        "logs": [(lv, dec(t)) for lv, t in d["logs"]],
+        "final": {int(k): (dec(v[0]), v[1], v[2]) for k, v in d["final"].items()},
+    }

@@ -1,0 +1,187 @@
+"""GPU: the dead-downstream side effect (sr-main.c:106) and the on-device per-downstream MTU packing
+(push_to_downstream + ds_schedule_flush, sr-main.c:49-83) through the C ABI, bit for bit against the
+oracle's restatements (which tests/test_oracle_router.py pins to the compiled reference)."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+from conftest import load_case
+
+pytestmark = pytest.mark.gpu
+
+
+def _dead(n, frac, seed):
+    rng = np.random.default_rng(seed)
+    alive = np.ones(n, dtype=int)
+    k = int(round(frac * n))
+    if k:
+        alive[rng.choice(n, k, replace=False)] = 0
+    return alive.tolist()
+
+
+STREAMS = [
+    # (line lengths, n_downstreams, dead fraction, p_invalid, bytes, seed)
+    ([64], 4, 0.0, 0.0, 1 << 20, 1),
+    ([64], 4, 0.25, 0.0, 1 << 20, 2),
+    ([256], 4, 0.25, 0.1, 1 << 20, 3),
+    ([1024], 16, 0.25, 0.0, 1 << 20, 4),
+    ([64, 256, 1024], 64, 0.25, 0.05, 1 << 20, 5),
+    ([64, 256, 1024], 64, 0.5, 0.0, 1 << 19, 6),   # > 16 dead: the wide probe kernel
+    ([6, 7, 13], 3, 0.0, 0.0, 1 << 19, 7),         # tiny lines: 241-line packets, multi-chunk shards
+    ([1449, 700, 6], 5, 0.2, 0.0, 1 << 19, 8),     # lines up to the 1449-byte limit
+    ([64], 1, 0.0, 0.0, 1 << 18, 9),
+    ([64, 256], 300, 0.3, 0.1, 1 << 19, 10),
+    ([64], 4, 1.0, 0.0, 1 << 16, 11),              # every downstream dead
+]
+
+
+@pytest.mark.parametrize("lens,n,dead,p_inv,nbytes,seed", STREAMS)
+def test_probed_dead_matches_oracle(pkg, oracle, lens, n, dead, p_inv, nbytes, seed):
+    s = pkg.gen_stream(nbytes, lens, seed=0xD00D + seed, p_invalid=p_inv)
+    alive = _dead(n, dead, seed)
+    with pkg.Router(n, nbytes) as r:
+        r.set_alive(alive)
+        recs, _, cnt = r.route(s.data)
+        got = r.last_probed_dead()
+    want = oracle.probed_dead(s.data, n, alive)
+    assert cnt == s.n_lines
+    assert got.tolist() == want.tolist()
+    assert all(alive[k] == 0 for k in got)
+
+
+@pytest.mark.parametrize("name", ["random_n4_s1", "random_n7_s8", "random_n64_s3", "random_n1000_s6",
+                                  "edge_n3_mid_dead", "edge_n4_all_dead"])
+def test_probed_dead_golden(pkg, oracle, name):
+    """Against the compiled reference's own drop (tests/golden/probed_dead.json via the harness)."""
+    import json
+    import os
+
+    from conftest import GOLDEN
+
+    case = load_case(name)
+    want = json.load(open(os.path.join(GOLDEN, "probed_dead.json")))[name]
+    data = pkg.frame_datagrams(case["dgrams"])
+    with pkg.Router(case["n"], max(len(data), 1)) as r:
+        r.set_alive(case["alive"].astype(np.uint64))
+        r.route(data)
+        got = r.last_probed_dead()
+    assert got.tolist() == want
+
+
+def _check_pack(pkg, oracle, data, n, alive, fill, r):
+    srt, pk, fo, nv, pr = r.route_pack(data, fill)
+    recs, _, _ = oracle.route(data, n, alive)
+    probed = oracle.probed_dead(data, n, alive)
+    srt_o, pk_o, fo_o, nv_o = oracle.pack_packets(recs, n, fill, probed)
+    assert pr.tolist() == probed.tolist()
+    assert nv == nv_o
+    assert np.array_equal(srt, srt_o), "sorted records differ"
+    assert len(pk) == len(pk_o), (len(pk), len(pk_o))
+    assert np.array_equal(pk.view(np.uint8), pk_o.view(np.uint8)), "packet descriptors differ"
+    assert np.array_equal(fo, fo_o), "pending bytes after the batch differ"
+    return srt, pk, fo
+
+
+@pytest.mark.parametrize("lens,n,dead,p_inv,nbytes,seed", STREAMS)
+def test_route_pack_matches_oracle(pkg, oracle, lens, n, dead, p_inv, nbytes, seed):
+    s = pkg.gen_stream(nbytes, lens, seed=0xFACE + seed, p_invalid=p_inv)
+    alive = _dead(n, dead, seed)
+    rng = np.random.default_rng(seed)
+    with pkg.Router(n, nbytes) as r:
+        r.set_alive(alive)
+        for fill in (None, rng.integers(0, 1451, n).tolist(), [1450] * n, [1] * n):
+            _check_pack(pkg, oracle, s.data, n, alive, fill, r)
+
+
+def test_route_pack_chained_batches(pkg, oracle):
+    """Pending bytes carried across batches, alive toggles in between; materialised packet bytes
+    equal the oracle's."""
+    n = 6
+    rng = np.random.default_rng(3)
+    fill_g = [0] * n
+    fill_o = [0] * n
+    pend_g, pend_o = {}, {}
+    with pkg.Router(n, 1 << 18) as r:
+        for b in range(12):
+            alive = (rng.random(n) > 0.3).astype(int).tolist()
+            s = pkg.gen_stream(int(rng.integers(1000, 1 << 18)), [6, 64, 300, 1449], seed=100 + b, p_invalid=0.05)
+            r.set_alive(alive)
+            srt, pk, fill_g, _, _ = r.route_pack(s.data, fill_g)
+            out_g, pend_g = oracle.materialize(s.data, srt, pk, pend_g, fill_g)
+            recs, _, _ = oracle.route(s.data, n, alive)
+            srt_o, pk_o, fill_o, _ = oracle.pack_packets(recs, n, fill_o, oracle.probed_dead(s.data, n, alive))
+            out_o, pend_o = oracle.materialize(s.data, srt_o, pk_o, pend_o, fill_o)
+            assert out_g == out_o
+            assert pend_g == pend_o
+            assert [len(pend_g.get(k, b"")) for k in range(n)] == list(map(int, fill_g))
+
+
+def test_pack_packets_device_many(pkg, oracle, torch_stream):
+    """Several batches routed in one sr_route_device_many launch (with probed-dead bitmaps), then
+    sr_pack_packets per batch on device buffers, the pending bytes chained on the device."""
+    import torch
+
+    n, nb, size = 8, 5, 1 << 20
+    alive = [1, 1, 0, 1, 1, 0, 1, 1]
+    streams = [pkg.gen_stream(size, [64, 256, 1024], seed=700 + b, p_invalid=0.05) for b in range(nb)]
+    cap = max(s.n_lines for s in streams)
+    d_in = torch.zeros((nb, size), dtype=torch.uint8, device="cuda")
+    for b, s in enumerate(streams):
+        d_in[b, : s.data.size].copy_(torch.from_numpy(s.data))
+    d_rec = torch.zeros((nb, cap), dtype=torch.int64, device="cuda")
+    d_cnt = torch.zeros(nb, dtype=torch.int64, device="cuda")
+    d_pd = torch.zeros((nb, 1), dtype=torch.int64, device="cuda")
+    mp = pkg.max_packets(size, n)
+    d_srt = torch.zeros((nb, cap), dtype=torch.int64, device="cuda")
+    d_pk = torch.zeros((nb, mp * 2), dtype=torch.int64, device="cuda")
+    d_counts = torch.zeros((nb, 3), dtype=torch.int64, device="cuda")
+    d_fill = torch.zeros((nb + 1, n), dtype=torch.int16, device="cuda")
+    d_fill[0] = torch.tensor([5, 1450, 0, 700, 64, 3, 1449, 0], dtype=torch.int16)
+    with pkg.Router(n, size) as r:
+        r.set_alive(alive)
+        r.set_stream(torch_stream.cuda_stream)
+        r.route_device_many([(d_in[b].data_ptr(), int(s.data.size), d_rec[b].data_ptr(), cap, None,
+                              d_cnt[b].data_ptr(), d_pd[b].data_ptr()) for b, s in enumerate(streams)])
+        for b in range(nb):
+            r.pack_packets(d_rec[b].data_ptr(), d_cnt[b].data_ptr(), cap, d_fill[b].data_ptr(), d_pd[b].data_ptr(),
+                           d_srt[b].data_ptr(), d_pk[b].data_ptr(), mp, d_counts[b].data_ptr(),
+                           d_fill[b + 1].data_ptr())
+        torch.cuda.synchronize()
+    fill = d_fill[0].cpu().numpy().view(np.uint16).tolist()
+    for b, s in enumerate(streams):
+        recs, _, cnt = oracle.route(s.data, n, alive)
+        probed = oracle.probed_dead(s.data, n, alive)
+        pd = np.frombuffer(d_pd[b].cpu().numpy().tobytes(), dtype=np.uint64)
+        assert pkg.bitmap_shards(pd, n).tolist() == probed.tolist()
+        srt_o, pk_o, fill_o, nv = oracle.pack_packets(recs, n, fill, probed)
+        np_, nv_g, nl = d_counts[b].cpu().tolist()
+        assert (np_, nv_g, nl) == (len(pk_o), nv, cnt)
+        srt = np.frombuffer(d_srt[b].cpu().numpy().tobytes(), dtype=pkg.RECORD_DTYPE)[:cnt]
+        pk = np.frombuffer(d_pk[b].cpu().numpy().tobytes(), dtype=pkg.PACKET_DTYPE)[:np_]
+        assert np.array_equal(srt, srt_o)
+        assert np.array_equal(pk.view(np.uint8), pk_o.view(np.uint8))
+        got_fill = d_fill[b + 1].cpu().numpy().view(np.uint16).tolist()
+        assert got_fill == fill_o.tolist()
+        fill = got_fill
+
+
+def test_route_pack_edges(pkg, oracle):
+    """Exact-fit packets, carry-only flushes, empty and single-line batches."""
+    n = 2
+    with pkg.Router(n, 1 << 16) as r:
+        cases = [
+            b"",
+            b"a:1|c\n",
+            (b"x" * 1443 + b":1|c\n"),                    # 1449 bytes: one line per packet
+            (b"y" * 720 + b":1|c\n") * 2,                 # two 726-byte lines: 1452 > 1450
+            (b"z" * 719 + b":1|c\n") * 2,                 # two 725-byte lines: exactly 1450
+            b"bad\n" + b"k:1|c\n" * 500 + b"nocolon_line\n",
+        ]
+        for data in cases:
+            for fill in ([0, 0], [1450, 1450], [1449, 1], [725, 724]):
+                if not data:
+                    srt, pk, fo, nv, pr = r.route_pack(data, fill)
+                    assert len(srt) == 0 and len(pk) == 0 and fo.tolist() == fill
+                    continue
+                _check_pack(pkg, oracle, data, n, None, fill, r)

@@ -1,0 +1,70 @@
+"""GPU: one router data thread (include/sr_router.h: host C over the C ABI, per-line work and MTU
+packing on the device) replays the scripted sessions the compiled reference ran
+(tests/golden/router_*.json): every packet each downstream received, every WARN line, the final
+pending buffers and counters must be identical, whether each datagram is its own batch or
+consecutive datagrams share one."""
+from __future__ import annotations
+
+import importlib
+
+import pytest
+
+from conftest import load_router_fixture, router_fixtures
+
+pytestmark = pytest.mark.gpu
+
+
+def _replay(pkg, f, group: int, in_place: bool):
+    core_mod = importlib.import_module("statsd-router_amd.core")
+    core = core_mod.Core(f["n"], f["ds_hosts"], f["ds_data_ports"], f["ping_prefix"], f["hostname"], f["data_port"],
+                         max_batch_bytes=1 << 20)
+    pend = []
+
+    def flush_batch():
+        if pend:
+            framed = pkg.frame_datagrams(pend)
+            (core.route_in_place if in_place else core.route)(framed)
+            pend.clear()
+
+    for e in f["events"]:
+        if e[0] == "dgram":
+            pend.append(e[1])
+            if len(pend) >= group:
+                flush_batch()
+            continue
+        flush_batch()
+        if e[0] == "alive":
+            core.set_alive(e[1])
+        elif e[0] == "flush":
+            core.flush_timer()
+        elif e[0] == "ping":
+            core.ping()
+    flush_batch()
+    final = {s: core.state(s) for s in range(f["n"])}
+    core.close()
+    return core, final
+
+
+@pytest.mark.parametrize("group", [1, 7, 1000])
+@pytest.mark.parametrize("name", router_fixtures())
+def test_core_replays_reference_session(pkg, name, group):
+    f = load_router_fixture(name)
+    core, final = _replay(pkg, f, group, in_place=group == 7)
+    assert core.logs == f["logs"]
+    assert {k: v for k, v in core.packets.items() if v} == f["packets"]
+    assert final == f["final"]
+
+
+def test_core_metric_names_match_oracle(pkg):
+    import sr_router_oracle as RO
+
+    core_mod = importlib.import_module("statsd-router_amd.core")
+    hosts = ["10.0.0.100", "db.example", "a.b", "host-with-long.name.example.com"]
+    ports = ["8125", "9", "65535", "1"]
+    with core_mod.Core(4, hosts, ports, "statsd.prefix", "router-7", 9003) as c:
+        t = RO.DataThread(4, hosts, ports, "statsd.prefix", "router-7", 9003)
+        for i in range(4):
+            assert c.metric_name(i, 0) == t.conn[i]
+            assert c.metric_name(i, 1) == t.traffic_name[i]
+            assert c.metric_name(i, 2) == t.packet_name[i]
+        assert c.metric_name(0, 3) == t.alive_metric
