@@ -1,0 +1,160 @@
+"""Test helpers: run a statsd-router executable (ours, statsd-router_amd/bin/statsd-router-mi355x, or the
+reference's, oracle/_ref/statsd-router compiled from /root/reference) on a config file, collect its
+log lines, talk to its ports. Mirrors the reference test library's harness
+(statsd-router-test-lib.rb: config writer :296-306, popen + OutputHandler :170-181, mocks :45-167)."""
+from __future__ import annotations
+
+import os
+import re
+import socket
+import subprocess
+import threading
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OURS = os.path.join(REPO, "statsd-router_amd", "bin", "statsd-router-mi355x")
+REFERENCE = os.path.join(REPO, "oracle", "_ref", "statsd-router")
+LOG_RE = re.compile(rb"^\d{4}-\d\d-\d\d \d\d:\d\d:\d\d -?\d+ (TRACE|DEBUG|INFO|WARN|ERROR) (.*)$", re.S)
+
+
+def free_ports(k: int, step: int = 1) -> int:
+    """A base port such that base, base+step, ... (k ports, TCP and UDP) are free on 127.0.0.1."""
+    for _ in range(200):
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        base = s.getsockname()[1]
+        s.close()
+        if base + k * step >= 65000:
+            continue
+        ok = True
+        for i in range(k * step):
+            for typ in (socket.SOCK_STREAM, socket.SOCK_DGRAM):
+                t = socket.socket(socket.AF_INET, typ)
+                try:
+                    t.bind(("127.0.0.1", base + i))
+                except OSError:
+                    ok = False
+                finally:
+                    t.close()
+        if ok:
+            return base
+    raise RuntimeError("no free port range")
+
+
+def config_text(data_port, control_port, downstreams, log_level=1, threads=1, flush=0.2, health=0.2, ping=10.0,
+                prefix="statsd-cluster-test"):
+    ds = ",".join(f"127.0.0.1:{d}:{h}" for d, h in downstreams)
+    return (f"data_port={data_port}\ncontrol_port={control_port}\ndownstream_flush_interval={flush}\n"
+            f"downstream_health_check_interval={health}\ndownstream_ping_interval={ping}\n"
+            f"ping_prefix={prefix}\ndownstream={ds}\nlog_level={log_level}\nthreads_num={threads}\n")
+
+
+class Router:
+    """A running router; .lines = [(level, message bytes)] parsed from its stdout."""
+
+    def __init__(self, exe: str, config: str, tmpdir: str, env=None):
+        self.cfg = os.path.join(tmpdir, f"sr-{os.path.basename(exe)}-{time.monotonic_ns()}.conf")
+        with open(self.cfg, "w") as f:
+            f.write(config)
+        self.p = subprocess.Popen([exe, self.cfg], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                  env=dict(os.environ, **(env or {})))
+        self.raw: list[bytes] = []
+        self.lines: list[tuple[str, bytes]] = []
+        self._cv = threading.Condition()
+        self._t = threading.Thread(target=self._reader, daemon=True)
+        self._t.start()
+
+    def _reader(self):
+        for line in self.p.stdout:
+            line = line.rstrip(b"\n")
+            with self._cv:
+                self.raw.append(line)
+                m = LOG_RE.match(line)
+                if m:
+                    self.lines.append((m.group(1).decode(), m.group(2)))
+                self._cv.notify_all()
+
+    def wait_for(self, pred, timeout=20.0) -> bool:
+        end = time.monotonic() + timeout
+        with self._cv:
+            while True:
+                if any(pred(lv, msg) for lv, msg in self.lines):
+                    return True
+                left = end - time.monotonic()
+                if left <= 0 or (self.p.poll() is not None and not self._t.is_alive()):
+                    return any(pred(lv, msg) for lv, msg in self.lines)
+                self._cv.wait(min(left, 0.2))
+
+    def wait_exit(self, timeout=10.0) -> int:
+        rc = self.p.wait(timeout)
+        self._t.join(timeout)
+        return rc
+
+    def stop(self):
+        if self.p.poll() is None:
+            self.p.terminate()
+            try:
+                self.p.wait(5)
+            except subprocess.TimeoutExpired:
+                self.p.kill()
+                self.p.wait(5)
+        self._t.join(5)
+
+
+class HealthServer:
+    """TCP health endpoint of a mock downstream: "health" -> "health: up\\n" while started
+    (statsd-router-test-lib.rb:104-119)."""
+
+    def __init__(self, port: int):
+        self.port = port
+        self.sock = None
+        self._stop = threading.Event()
+        self._t = None
+
+    def start(self):
+        self.sock = socket.socket()
+        self.sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        self.sock.bind(("127.0.0.1", self.port))
+        self.sock.listen(16)
+        self.sock.settimeout(0.1)
+        self._stop.clear()
+        self._t = threading.Thread(target=self._serve, daemon=True)
+        self._t.start()
+
+    def _serve(self):
+        conns = []
+        while not self._stop.is_set():
+            try:
+                c, _ = self.sock.accept()
+                c.settimeout(0.05)
+                conns.append(c)
+            except OSError:
+                pass
+            for c in list(conns):
+                try:
+                    d = c.recv(64)
+                    if not d:
+                        conns.remove(c)
+                        c.close()
+                        continue
+                    c.sendall(b"health: up\n")
+                except socket.timeout:
+                    pass
+                except OSError:
+                    conns.remove(c)
+        for c in conns:
+            c.close()
+
+    def stop(self):
+        self._stop.set()
+        if self._t:
+            self._t.join(2)
+        if self.sock:
+            self.sock.close()
+            self.sock = None
+
+
+def control(port: int, request: bytes, timeout=3.0) -> bytes:
+    with socket.create_connection(("127.0.0.1", port), timeout=timeout) as s:
+        s.sendall(request)
+        return s.recv(64)
