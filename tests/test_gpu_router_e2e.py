@@ -97,7 +97,8 @@ def run_router(exe, datagrams, n_ds, tmp, threads=1):
         for line in pkt.split(b"\n")[:-1]:
             if not line.startswith(PREFIX.encode()):
                 got[d][line + b"\n"] += 1
-    warns = [m for lv, m in r.lines if lv == "WARN"]
+    data_path = (b"udp_read_cb:", b"process_data_line:", b"find_downstream:")
+    warns = [m for lv, m in r.lines if lv == "WARN" and m.startswith(data_path)]
     return got, warns
 
 

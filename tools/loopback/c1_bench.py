@@ -26,7 +26,7 @@ BLAST = os.path.join(HERE, "sr_blast")
 SINK = os.path.join(HERE, "sr_sink")
 
 
-def run(exe, seconds, threads, rate, dgram, tmp, env=None):
+def run(exe, seconds, threads, rate, dgram, tmp, env=None, nblast=1):
     base = free_ports(6)
     data_port, ctl, sink_base = base, base + 1, base + 2
     sink = subprocess.Popen([SINK, str(sink_base), "1", str(seconds + 30), "1.5"], stdout=subprocess.PIPE,
@@ -38,9 +38,11 @@ def run(exe, seconds, threads, rate, dgram, tmp, env=None):
         if not r.wait_for(lambda lv, m: m == b"ds_health_read_cb downstream 0 is up", 30):
             raise RuntimeError(f"{exe}: downstream never came up: {r.raw[-10:]}")
         time.sleep(0.5)
-        b = subprocess.run([BLAST, str(data_port), str(seconds), str(rate), str(dgram)], capture_output=True,
-                           timeout=seconds + 30)
-        sent = json.loads(b.stdout)
+        blasters = [subprocess.Popen([BLAST, str(data_port), str(seconds), str(rate), str(dgram), str(17 + k)],
+                                     stdout=subprocess.PIPE) for k in range(nblast)]
+        outs = [json.loads(b.communicate(timeout=seconds + 30)[0]) for b in blasters]
+        sent = {k: sum(o[k] for o in outs) for k in ("datagrams", "lines", "bytes")}
+        sent["seconds"] = max(o["seconds"] for o in outs)
         out, _ = sink.communicate(timeout=seconds + 60)
         got = json.loads(out)
     finally:
@@ -49,7 +51,7 @@ def run(exe, seconds, threads, rate, dgram, tmp, env=None):
             sink.kill()
     span = max(got["last"] - got["first"], 1e-9)
     return {
-        "router": os.path.basename(exe), "threads_num": threads, "seconds": sent["seconds"],
+        "router": os.path.basename(exe), "threads_num": threads, "blasters": nblast, "seconds": sent["seconds"],
         "offered_lines_per_s": round(sent["lines"] / sent["seconds"], 1),
         "offered_datagrams_per_s": round(sent["datagrams"] / sent["seconds"], 1),
         "delivered_lines": got["lines"], "delivered_lines_per_s": round(got["lines"] / span, 1),
@@ -65,6 +67,7 @@ def main():
     ap.add_argument("--rate", type=float, default=0.0)
     ap.add_argument("--dgram", type=int, default=1400)
     ap.add_argument("--only", choices=["ours", "reference"], default=None)
+    ap.add_argument("--blasters", type=int, default=1, help="sender processes")
     a = ap.parse_args()
     import tempfile
 
@@ -73,7 +76,7 @@ def main():
         for tag, exe in exes:
             if a.only and tag != a.only:
                 continue
-            print(json.dumps(dict(run(exe, a.seconds, a.threads, a.rate, a.dgram, tmp), kind=tag)), flush=True)
+            print(json.dumps(dict(run(exe, a.seconds, a.threads, a.rate, a.dgram, tmp, nblast=a.blasters), kind=tag)), flush=True)
 
 
 if __name__ == "__main__":

@@ -126,20 +126,24 @@ int main(int argc, char **argv) {
                 close(c);
             }
         }
-        for (int i = 0; i < nconn; i++) {
-            if (!(pf[2 * n + i].revents & (POLLIN | POLLHUP))) continue;
+        /* health connections (persistent, like the reference's health client keeps them): poll
+         * indices were taken before any accept above, so walk the polled ones by index and compact
+         * after */
+        const int polled = np - 2 * n;
+        for (int i = 0; i < polled; i++) {
+            if (!(pf[2 * n + i].revents & (POLLIN | POLLHUP | POLLERR))) continue;
             char req[64];
             ssize_t r = recv(conn[i], req, sizeof(req), 0);
-            if (r <= 0) {
+            if (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR)) continue;
+            if (r <= 0 || send(conn[i], "health: up\n", 11, MSG_NOSIGNAL) < 0) {
                 close(conn[i]);
-                conn[i--] = conn[--nconn];
-                continue;
-            }
-            if (send(conn[i], "health: up\n", 11, MSG_NOSIGNAL) < 0) {
-                close(conn[i]);
-                conn[i--] = conn[--nconn];
+                conn[i] = -1;
             }
         }
+        int k = 0;
+        for (int i = 0; i < nconn; i++)
+            if (conn[i] >= 0) conn[k++] = conn[i];
+        nconn = k;
     }
     if (dump) fclose(dump);
     uint64_t td = 0, tl = 0, tb = 0;
