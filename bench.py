@@ -347,19 +347,67 @@ def verify_timed_launch(pkg, graph, stream, d_out, host, M, max_lines, shards, a
 
 
 def cpu_baseline(host, shards, alive, seconds):
-    """The C restatement (oracle/sr_oracle.c, calibrated against the compiled reference in
-    BASELINE.md) routing the same batches on this host: 1 thread, and one thread per CPU of the
-    process's share, each thread one reference data thread (threads_num, sr-main.c:363-367)."""
+    """The reference's own read callback (oracle/_ref/sr_ref_bench: sr-main.c's udp_read_cb compiled
+    unmodified from /root/reference, log_level ERROR, lines pushed into real downstream buffers,
+    each datagram through a socketpair recv) on this host's CPUs: one process alone, then one per
+    CPU of the process's share in parallel, each a reference data thread (threads_num,
+    sr-main.c:363-367). Without that binary, the C restatement (oracle/sr_oracle.c, measured
+    1.3-1.6x faster than the reference) is timed instead ("kind": "port")."""
+    import struct
+    import subprocess
+    import tempfile
+
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import sr_oracle
 
-    sample = [host[b].data for b in range(min(4, len(host)))]
     affinity = len(os.sched_getaffinity(0))
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     cores = min(affinity, share) if share > 0 else affinity
+    common = {"cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+              "cores_note": (f"threads = the process's CPU share (sched_getaffinity {affinity}, OMP_NUM_THREADS "
+                             f"{share or 'unset'}); on the GPU box that share is 16 CPUs per GPU")}
+    ref = os.path.join(REPO, "oracle", "_ref", "sr_ref_bench")
+    if os.path.exists(ref):
+        h = host[0]
+        with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+            off = 0
+            for l in h.dgram_lens.tolist():
+                f.write(struct.pack("<I", l))
+                f.write(h.data[off:off + l].tobytes())
+                off += l
+            path = f.name
+        try:
+            def launch(k):
+                return [subprocess.Popen([ref, str(shards), path, str(seconds)], stdout=subprocess.PIPE) for _ in range(k)]
+
+            def collect(ps):
+                return [json.loads(p.communicate(timeout=4 * seconds + 60)[0]) for p in ps]
+
+            one = collect(launch(1))[0]
+            many = collect(launch(cores))
+        finally:
+            os.unlink(path)
+        lines_bytes = h.data.size / max(h.n_lines, 1)
+        tot = sum(r["reference_lines_per_s"] for r in many)
+        return dict({
+            "value": round(tot / 1e6, 3),
+            "unit": "M metrics/s",
+            "cores": cores,
+            "kind": "reference",
+            "sample": (f"one 16 MiB batch of the same workload ({h.n_lines} lines in {len(h.dgram_lens)} datagrams) "
+                       f"replayed through the reference's udp_read_cb (oracle/_ref/sr_ref_bench), {cores} processes x "
+                       f"{seconds:.1f} s = {cores * seconds:.0f} core-seconds"),
+            "single_thread": round(one["reference_lines_per_s"] / 1e6, 3),
+            "single_thread_gib_per_s": round(one["reference_lines_per_s"] * lines_bytes / 2**30, 3),
+            "gib_per_s": round(tot * lines_bytes / 2**30, 3),
+            "restatement_single_thread": round(one["restatement_lines_per_s"] / 1e6, 3),
+            "restatement_over_reference": one["restatement_over_reference"],
+        }, **common)
+
+    sample = [host[b].data for b in range(min(4, len(host)))]
     l1, b1, w1 = sr_oracle.bench(sample, shards, alive, 1, seconds)
     lm, bm, wm = sr_oracle.bench(sample, shards, alive, cores, seconds)
-    return {
+    return dict({
         "value": round(lm / wm / 1e6, 3),
         "unit": "M metrics/s",
         "cores": cores,
@@ -370,11 +418,7 @@ def cpu_baseline(host, shards, alive, seconds):
         "single_thread": round(l1 / w1 / 1e6, 3),
         "single_thread_gib_per_s": round(b1 / w1 / 2**30, 3),
         "gib_per_s": round(bm / wm / 2**30, 3),
-        "cpu_model": cpu_model(),
-        "host_cpus": os.cpu_count(),
-        "cores_note": (f"threads = the process's CPU share (sched_getaffinity {affinity}, OMP_NUM_THREADS "
-                       f"{share or 'unset'}); on the GPU box that share is 16 CPUs per GPU"),
-    }
+    }, **common)
 
 
 def regroup_leg(pkg, dev, local, world, rank, cfg, steps):

@@ -24,7 +24,8 @@ import numpy as np
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_DIR = os.path.join(PKG_DIR, "lib")
-ROUTE_LIB = os.path.join(LIB_DIR, "libsr_route.so")
+# SR_ROUTE_LIB: another build of the same library (same-box A/B runs of kernel variants, tools/ab_kernels.sh)
+ROUTE_LIB = os.environ.get("SR_ROUTE_LIB") or os.path.join(LIB_DIR, "libsr_route.so")
 GEN_LIB = os.path.join(LIB_DIR, "libsr_gen.so")
 HEADER = os.path.join(REPO_DIR, "include", "sr_route.h")
 

@@ -62,7 +62,6 @@ static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream
     static const int v = [] {
         const char *e = getenv("SR_VARIANT");
         if (!e || !*e) return 0;
-        if (!strcmp(e, "mixed_lanes")) return 13;
         if (!strcmp(e, "no_mid_base")) return 14;
         // upper bounds, not routing (records wrong or missing; line counts still exact)
         if (!strcmp(e, "fake_base")) return 7;
@@ -71,7 +70,6 @@ static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream
         return 0;
     }();
     switch (v) {
-    case 13: return launch_route<kBlock, ABL_MIXED_LANES>(ds, p, stream);
     case 14: return launch_route<kBlock, ABL_NO_MID_BASE>(ds, p, stream);
     case 7: return launch_route<kBlock, ABL_FAKE_BASE>(ds, p, stream);
     case 8: return launch_route<kBlock, ABL_NO_HASH>(ds, p, stream);
