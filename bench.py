@@ -70,7 +70,7 @@ def parse(argv=None):
     ap.add_argument("--regroup", default="auto", choices=["auto", "on", "off"],
                     help="classify + all-to-all regroup leg (auto: on when more than one GPU)")
     ap.add_argument("--regroup-config", default="c5", choices=sorted(CONFIGS))
-    ap.add_argument("--regroup-steps", type=int, default=16)
+    ap.add_argument("--regroup-steps", type=int, default=8)
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -421,11 +421,12 @@ def cpu_baseline(host, shards, alive, seconds):
     }, **common)
 
 
-def regroup_leg(pkg, dev, local, world, rank, cfg, steps):
+def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8):
     """Classify + regroup on its own batches of config `cfg` (C5 by default: mixed
-    lengths, 64 shards): per batch, route, pack by owner GPU (shard % G) and all-to-all the packed
-    lines and records (RCCL over xGMI). Not graph-captured: the split sizes go through the host.
-    Timed like the main region (barrier + synchronize, max over ranks)."""
+    lengths, 64 shards). One step = one route launch of `per_step` batches, then ONE pack of all of
+    them by owner GPU (shard % G, sr_pack_many_by_owner) and ONE exchange: an all-to-all of the
+    split sizes (the step's single host round trip), of the packed lines and of the records (RCCL
+    over xGMI). Timed like the main region (barrier + synchronize, max over ranks)."""
     import torch
     import torch.distributed as dist
 
@@ -433,7 +434,7 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps):
     if world == 1 and not dist.is_initialized():
         dist.init_process_group("nccl", store=dist.TCPStore("127.0.0.1", 0, 1, True), rank=0, world_size=1)
     desc, batch_bytes, lens, p_inv, shards, seed0, _ = CONFIGS[cfg]
-    nb = 4
+    nb = per_step
     host = [pkg.gen_stream(batch_bytes, lens, seed=seed0 + 1_000_003 * rank + 65_537 * b, p_invalid=p_inv)
             for b in range(nb)]
     sizes = [int(s.data.size) for s in host]
@@ -445,56 +446,47 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps):
     stream = torch.cuda.Stream(device=dev)
     router = pkg.Router(shards, batch_bytes, device=local)
     router.set_stream(stream.cuda_stream)
-    d_rec = torch.empty(max_lines, dtype=torch.int64, device=dev)
-    d_n = torch.zeros(1, dtype=torch.int64, device=dev)
+    d_rec = torch.empty((nb, max_lines), dtype=torch.int64, device=dev)
+    d_n = torch.zeros(nb, dtype=torch.int64, device=dev)
     base = d_in.data_ptr()
+    route_descs = [(base + b * batch_bytes, sizes[b], d_rec[b].data_ptr(), max_lines, None, d_n[b].data_ptr())
+                   for b in range(nb)]
+    pack_descs = [(base + b * batch_bytes, sizes[b], d_rec[b].data_ptr(), max_lines, d_n[b].data_ptr())
+                  for b in range(nb)]
 
     with torch.cuda.stream(stream):
-        reg = rg_mod.Regrouper(pkg, router, batch_bytes, max_lines, slots=2)
+        reg = rg_mod.LaunchRegrouper(pkg, router, sum(sizes), nb * max_lines)
 
-        def start(i):
-            b = i % nb
-            router.route_device(base + b * batch_bytes, sizes[b], d_rec.data_ptr(), max_lines, None, d_n.data_ptr())
-            reg.start(i % 2, base + b * batch_bytes, sizes[b], d_rec.data_ptr(), d_n.data_ptr(), max_lines)
-
-        def finish(i):
-            rb, rr, _ = reg.finish(i % 2)
-            # bytes this rank sent to the other ranks, from the host copy the exchange already made
+        def step():
+            router.route_device_many(route_descs)
+            rb, rr, _ = reg(pack_descs)
             sent = sum(c[1] for c in reg.last_sent) - reg.last_sent[rank][1]
             return int(rr.numel()), int(rb.numel()), sent
 
-        def run(n):
-            # two slots: batch i+1 is routed and packed while the host waits for batch i's split sizes
-            acc = [0, 0, 0]
-            start(0)
-            for i in range(n):
-                if i + 1 < n:
-                    start(i + 1)
-                acc = [a + x for a, x in zip(acc, finish(i))]
-            return acc
-
-        run(2)
+        for _ in range(2):
+            step()
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        recv_lines, recv_bytes, sent_off = run(steps)
+        acc = [0, 0, 0]
+        for _ in range(steps):
+            acc = [a + x for a, x in zip(acc, step())]
         torch.cuda.synchronize()
         dist.barrier()
         wall = time.perf_counter() - t0
     router.close()
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    tot = torch.tensor([sum(lines[i % nb] for i in range(steps)), recv_lines, recv_bytes, sent_off],
-                       dtype=torch.float64, device=dev)
+    tot = torch.tensor([sum(lines) * steps, acc[0], acc[1], acc[2]], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     w = float(t[0])
     return {"value": round(float(tot[0]) / w / 1e6, 3), "unit": "M metrics/s", "workload": desc,
-            "steps_per_gpu": steps, "ms_per_step": round(w * 1e3 / steps, 4),
+            "steps_per_gpu": steps, "batches_per_step": nb, "ms_per_step": round(w * 1e3 / steps, 4),
             "lines_regrouped": int(tot[1]), "bytes_regrouped": int(tot[2]),
             "bytes_sent_to_other_gpus_per_s": round(float(tot[3]) / w / 1e9, 3),
-            "note": (f"route + sr_pack_by_owner + all-to-all (split sizes, packed lines, records) per 16 MiB batch "
-                     f"over {world} GPU(s); owner = shard % {world}; host round trip for the split sizes, "
-                     f"two slots: batch i+1 routed and packed while batch i's sizes come back")}
+            "note": (f"route launch of {nb} x 16 MiB batches + one sr_pack_many_by_owner + one exchange (split sizes, "
+                     f"packed lines, records) per step over {world} GPU(s); owner = shard % {world}; one host round "
+                     f"trip per step for the split sizes")}
 
 
 def e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M, groups=24):

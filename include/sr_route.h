@@ -155,6 +155,15 @@ int sr_pack_by_owner(sr_ctx *ctx, const uint8_t *d_bytes, size_t nbytes, const s
                      uint8_t *d_out_bytes, size_t out_cap, sr_record *d_out_recs,
                      uint64_t *d_owner_counts);
 
+/* sr_pack_by_owner over the batches of one route launch at once (one size exchange per launch):
+ * batches[j].d_bytes / nbytes / d_out (its records) / max_records / d_n_records as given to
+ * sr_route_device_many. Owner chunks hold batch 0's lines, then batch 1's, ..., each in input
+ * order; record offsets are relative to the owner's chunk. out_cap >= SR_PACK_CAPACITY(total
+ * bytes) (< 4 GiB), d_out_recs >= sum of max_records. count <= SR_MAX_BATCHES_PER_LAUNCH. */
+int sr_pack_many_by_owner(sr_ctx *ctx, const sr_batch *batches, size_t count, uint32_t n_owners,
+                          uint8_t *d_out_bytes, size_t out_cap, sr_record *d_out_recs,
+                          uint64_t *d_owner_counts);
+
 /* ---- per-downstream MTU packing ------------------------------------------ */
 /* push_to_downstream (sr-main.c:73-83) appends each routed line to its downstream's active buffer,
  * flushing the buffer first when the line would not fit in DOWNSTREAM_BUF_SIZE (1450) bytes

@@ -157,6 +157,29 @@ def materialize(data, sorted_recs: np.ndarray, packets: np.ndarray, pending: dic
     return out, new_pending
 
 
+def pack_many_by_owner(datas, recs_list, n_owners: int):
+    """sr_pack_many_by_owner restated from pack_by_owner: per owner, batch 0's chunk, then batch 1's, ...;
+    record offsets relative to the owner's chunk. Returns (packed bytes, packed records, counts[G, 2])."""
+    parts = [pack_by_owner(d, r, n_owners) for d, r in zip(datas, recs_list)]
+    out_b, out_r = [], []
+    counts = np.zeros((n_owners, 2), dtype=np.int64)
+    for o in range(n_owners):
+        shift = 0
+        for pb, pr, pc in parts:
+            l0 = int(pc[:o, 0].sum())
+            b0 = int(pc[:o, 1].sum())
+            nl, nb = int(pc[o, 0]), int(pc[o, 1])
+            out_b.append(pb[b0: b0 + nb])
+            rr = pr[l0: l0 + nl].copy()
+            rr["offset"] = rr["offset"] + shift
+            out_r.append(rr)
+            shift += nb
+            counts[o] += (nl, nb)
+    cat_b = np.concatenate(out_b) if out_b else np.zeros(0, np.uint8)
+    cat_r = np.concatenate(out_r) if out_r else np.zeros(0, RECORD_DTYPE)
+    return cat_b, cat_r, counts
+
+
 def bench(batches: Sequence[np.ndarray], n_downstreams: int, alive, threads: int, seconds: float):
     """Time the restatement (the reference's serial per-line loop) on host cores.
     Returns (lines, bytes, wall_seconds)."""

@@ -48,7 +48,7 @@ assert RECORD_DTYPE.itemsize == 8
 ABI_FUNCTIONS = (
     "sr_frame_datagram", "sr_frame_datagrams", "sr_open", "sr_set_alive", "sr_set_stream",
     "sr_route_batch", "sr_last_probed_dead", "sr_route_device", "sr_route_device_many", "sr_pack_by_owner",
-    "sr_pack_packets", "sr_route_pack_batch", "sr_alloc_host", "sr_free_host", "sr_sync", "sr_close", "sr_version",
+    "sr_pack_many_by_owner", "sr_pack_packets", "sr_route_pack_batch", "sr_alloc_host", "sr_free_host", "sr_sync", "sr_close", "sr_version",
 )
 SR_MAX_PACK_DOWNSTREAMS = 4096
 PACKET_DTYPE = np.dtype([("first", "<u4"), ("nlines", "<u2"), ("shard", "<u2"), ("length", "<u2"),
@@ -125,6 +125,8 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_route_device_many": (ctypes.c_int, [vp, ctypes.POINTER(SrBatch), ctypes.c_size_t]),
         "sr_pack_by_owner": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, ctypes.c_uint32,
                                             vp, ctypes.c_size_t, vp, vp]),
+        "sr_pack_many_by_owner": (ctypes.c_int, [vp, ctypes.POINTER(SrBatch), ctypes.c_size_t, ctypes.c_uint32, vp,
+                                                 ctypes.c_size_t, vp, vp]),
         "sr_pack_packets": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp, vp, vp, vp, ctypes.c_size_t, vp, vp]),
         "sr_route_pack_batch": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, c_size_p, c_size_p,
                                                vp, ctypes.c_size_t, c_size_p, vp]),
@@ -349,6 +351,16 @@ class Router:
         _check(self._lib.sr_pack_packets(self._h, vp(d_recs), vp(d_n_records), max_records, vp(d_fill_in or 0),
                                          vp(d_probed_dead or 0), vp(d_sorted), vp(d_packets), max_pk, vp(d_counts),
                                          vp(d_fill_out)), "sr_pack_packets")
+
+    def pack_many_by_owner(self, batches, n_owners: int, d_out_bytes: int, out_cap: int, d_out_recs: int,
+                           d_owner_counts: int) -> None:
+        """sr_pack_many_by_owner: batches = [(d_bytes, nbytes, d_recs, max_records, d_n_records), ...]."""
+        arr = (SrBatch * max(len(batches), 1))()
+        for i, (db, nb, dr, mr, dn) in enumerate(batches):
+            arr[i] = SrBatch(db, nb, dr, mr, None, dn, None)
+        vp = ctypes.c_void_p
+        _check(self._lib.sr_pack_many_by_owner(self._h, arr, len(batches), n_owners, vp(d_out_bytes), out_cap,
+                                               vp(d_out_recs), vp(d_owner_counts)), "sr_pack_many_by_owner")
 
     def sync(self) -> None:
         _check(self._lib.sr_sync(self._h), "sr_sync")

@@ -12,8 +12,9 @@
 // Lines routed to no shard (invalid length / format, all dead) are not packed: the GPU that
 // received them reports them (the WARN lines of sr-main.c:115,142,184 stay with the receiver).
 //
-// Three launches over tiles of kPackTile records: per-tile counts, one workgroup scanning them,
-// then the stable scatter (in-tile ranks recomputed with ballots and DPP scans).
+// Three launches over tiles of kPackTile records (the tiles of all packed batches in sequence):
+// per-tile counts, one workgroup scanning them, then the stable scatter (in-tile ranks recomputed
+// with ballots and DPP scans).
 #pragma once
 
 #include "route_kernel.hpp"
@@ -25,14 +26,24 @@ constexpr int kPackChunks = 8;                          // 256-record chunks per
 constexpr int kPackTile = kPackBlock * kPackChunks;     // records per tile
 constexpr int kMaxOwners = 64;
 
-struct PackParams {
+// One routed batch of a pack (up to kPackMaxBatches per pack: a route launch's batches are packed
+// and exchanged together, owner chunks holding batch 0's lines, then batch 1's, ...).
+constexpr int kPackMaxBatches = 32;
+struct PackBatch {
     const uint8_t *bytes;
-    uint32_t nbytes;
-    uint32_t n_owners;
     const sr_record *recs;
     const uint64_t *n_records;   // device line count written by the route kernel
+    uint32_t nbytes;
     uint32_t max_records;
-    uint32_t ntiles;
+    uint32_t tile0;              // first tile of the batch in the pack's tile sequence
+    uint32_t pad;
+};
+
+struct PackParams {
+    uint32_t nb;
+    uint32_t n_owners;
+    uint32_t ntiles;             // tiles of all batches
+    uint32_t pad;
     uint2 *tile_counts;          // [ntiles][n_owners] {lines, bytes} within the tile
     uint2 *tile_base;            // [ntiles][n_owners] exclusive prefix over tiles within the owner
     uint64_t *owner_start;       // [n_owners][2] {first line, first byte} of the owner's chunk
@@ -40,7 +51,16 @@ struct PackParams {
     uint8_t *out_bytes;
     uint64_t out_cap;
     sr_record *out_recs;
+    PackBatch b[kPackMaxBatches];
 };
+
+// the batch of pack tile `tile` and the tile's first record in it (nb <= 32: a scan over SGPRs)
+__device__ __forceinline__ const PackBatch &pack_batch_of(const PackParams &p, uint32_t tile, uint32_t &r0) {
+    uint32_t k = 0;
+    for (uint32_t j = 1; j < p.nb; ++j) k += tile >= p.b[j].tile0 ? 1u : 0u;
+    r0 = (tile - p.b[k].tile0) * kPackTile;
+    return p.b[k];
+}
 
 __device__ __forceinline__ uint32_t pack_len4(uint32_t len) { return (len + 3u) & ~3u; }
 
@@ -52,17 +72,18 @@ __device__ __forceinline__ int pack_owner(const sr_record &r, uint32_t n_owners)
 __global__ __launch_bounds__(kPackBlock) void pack_count_kernel(PackParams p) {
     __shared__ uint32_t s_lines[kMaxOwners], s_bytes[kMaxOwners];
     const int tid = threadIdx.x, lane = tid & 63;
-    const uint32_t n = (uint32_t)min(*p.n_records, (uint64_t)p.max_records);
+    uint32_t r0;
+    const PackBatch &bt = pack_batch_of(p, blockIdx.x, r0);
+    const uint32_t n = (uint32_t)min(*bt.n_records, (uint64_t)bt.max_records);
     const uint32_t G = p.n_owners;
     for (uint32_t o = tid; o < G; o += kPackBlock) s_lines[o] = s_bytes[o] = 0;
     __syncthreads();
-    const uint32_t r0 = blockIdx.x * kPackTile;
     for (int c = 0; c < kPackChunks; ++c) {
         const uint32_t i = r0 + c * kPackBlock + tid;
         int ow = -1;
         uint32_t len4 = 0;
         if (i < n) {
-            const sr_record r = p.recs[i];
+            const sr_record r = bt.recs[i];
             ow = pack_owner(r, G);
             len4 = pack_len4(r.length);
         }
@@ -137,19 +158,20 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
     __shared__ uint32_t s_wl[4][kMaxOwners], s_wb[4][kMaxOwners];   // per-wave chunk totals
     __shared__ uint32_t s_src[kPackBlock], s_dst[kPackBlock], s_len[kPackBlock];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t n = (uint32_t)min(*p.n_records, (uint64_t)p.max_records);
+    uint32_t r0;
+    const PackBatch &bt = pack_batch_of(p, blockIdx.x, r0);
+    const uint32_t n = (uint32_t)min(*bt.n_records, (uint64_t)bt.max_records);
     const uint32_t G = p.n_owners;
-    const uint32_t r0 = blockIdx.x * kPackTile;
     for (uint32_t o = tid; o < G; o += kPackBlock) s_run_l[o] = s_run_b[o] = 0;
     const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)p.bytes, (short)0, (int)p.nbytes, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)bt.bytes, (short)0, (int)bt.nbytes, 0x00020000);
     __syncthreads();
     for (int c = 0; c < kPackChunks; ++c) {
         const uint32_t i = r0 + c * kPackBlock + tid;
         int ow = -1;
         sr_record r{0, 0, 0};
         if (i < n) {
-            r = p.recs[i];
+            r = bt.recs[i];
             ow = pack_owner(r, G);
         }
         const uint32_t len4 = pack_len4(r.length);

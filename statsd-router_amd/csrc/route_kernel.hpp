@@ -77,6 +77,8 @@ enum : unsigned {
                              // the pipelined scanner publishes ahead of need)
     ABL_AGENT_GRANULES = 262144u,  // every count / base granule stored sc1 (round-1 v0.5), whatever the XCDs
     ABL_SCAN_SERIAL = 524288u,  // round-1 v0.6 scanner: 256 granules per round trip, one poll in flight
+    ABL_MIXED_LANES = 1048576u,  // per-line lane groups for tiles of mixed line lengths (opt-in: C5 -13 %,
+                                 // but its classification costs C2 / C4 2-5 % in registers)
     ABL_NO_MID_BASE = 2097152u,  // no base read part-way through the hash (round-1 v0.8)
     ABL_OLD_HASH = 1024u,   // round-1 v0.5 per-segment sdbm (v_alignbyte reads, compiler-extracted bytes)
 };
@@ -485,13 +487,10 @@ __device__ __noinline__ void note_all_dead(uint64_t *pd, uint32_t n) {
     }
 }
 
-constexpr uint32_t kLdsDeadBits = 1024;   // shards whose probed-dead bits a tile gathers in LDS
-
 // find_downstream (sr-main.c:86-117) for one line. Returns the shard, SR_ROUTE_ALL_DEAD, or
 // kRoutePending if more than kOverlay dead shards had to be probed. pd (may be null): the batch's
-// probed-dead bitmap; lpd: the tile's LDS copy of it when nds <= kLdsDeadBits (no-return LDS ors:
-// nothing waits and no result register is held in the probe loop), else null (global ors).
-__device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *pd, uint32_t *lpd) {
+// probed-dead bitmap.
+__device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *pd) {
     const uint32_t n = p.nds;
     if (p.dead >= n) {                                    // includes N == 0
         if (pd && n) note_all_dead(pd, n);
@@ -511,8 +510,7 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *pd, 
         for (int e = 0; e < kOverlay; ++e)
             if ((ov[e] >> 16) == j) k = ov[e] & 0xFFFFu;
         if (alive_bit(p.alive, k)) return k;                         // :101-104
-        if (lpd) atomicOr(&lpd[k >> 5], 1u << (k & 31));             // :106
-        else if (pd) __hip_atomic_fetch_or(pd + (k >> 6), 1ull << (k & 63), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (pd) note_dead(pd, k);                                    // :106
         if (j != i - 1) {                                            // :108-111
             uint32_t v = i - 1;
 #pragma unroll
@@ -546,14 +544,9 @@ struct SmemT {
     int32_t lend[kWin + 1];          // per staged line: tile position of its '\n'; slot 0 = previous
     int32_t lcol[kWin + 1];          // per staged line: first ':' in the tile part (kNone if none)
     uint32_t wave_cnt[kWaves];
-    // segment map of a mixed-length window: bit x = segment x is the first of its line; segpre[w] =
-    // set bits in words < w; segw[wave] = {segments, longest line's segments} of the wave's lines
-    static constexpr int kSegRounds = 1;                         // a window has < 2 * BLOCK segments
-    static constexpr int kSegWords = kSegRounds * BLOCK / 32;
-    uint32_t pdead[kLdsDeadBits / 32];   // probed dead shards of the tile's lines (flushed at the end)
-    uint32_t segbits[kSegWords];
-    uint16_t segpre[kSegWords];
-    uint32_t segw[kWaves][2];
+    uint32_t ccnt[kWaves][6];        // per wave: lines of the window per lane class
+    uint32_t ctab[6];                // per lane class: (first lane << 16) | first sorted slot
+    uint8_t lorder[kWin];            // the window's lines sorted by lane class, largest first
     uint32_t wave_scan[kWaves][4];   // per wave, inclusive at its last lane: '\n' count, latest '\n' lane, colon key
     uint64_t kp_lo[kPowLo];          // K^i
     uint64_t kp_hi[kPowHi];          // K^(64 i)
@@ -1126,8 +1119,6 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
     const BatchDesc &bd = p.b[bi];
     const uint32_t nbytes = bd.nbytes;
     const uint64_t *const base_slot = p.bases + bd.sbase + t;
-    // the tile's probed-dead bits gather in LDS (zeroed at entry), flushed once at the end
-    uint32_t *const lpd = (p.dead && bd.probed_dead && p.nds <= kLdsDeadBits) ? sm.pdead : nullptr;
     const int64_t T0 = (int64_t)t * kTileB;
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)nbytes, 0x00020000);
@@ -1291,62 +1282,29 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
             // (G * 64 < kTileB / tile_count, without the division)
             int G = 1;
             while (G < 32 && (G * 64 + 1) * (int)tile_count <= kTileB) G <<= 1;
-            // Geometry of window line jj: first byte s, '\n' at e, first ':' c (tile positions).
-            auto geom = [&](int jj, bool act, int &ls, int &le, int &lc) {
-                const int j = wbase + jj;
-                le = act ? sm.lend[jj + 1] : 0;
-                lc = act ? sm.lcol[jj + 1] : kNone;
-                if (j == 0 && c_pre != kNone) lc = c_pre;   // the straddling line's ':' lies before T0
-                ls = (j == 0) ? s_pre : (act ? sm.lend[jj] + 1 : 0);
-            };
-            // Verdict, shard and record of window line jj whose name hash is h (one lane per line).
-            auto record = [&](int jj, int ls, int le, int lc, uint64_t h) {
-                const int j = wbase + jj;
-                const int len = le - ls + 1;
-                uint32_t route;
-                if (!(len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH)) route = SR_ROUTE_INVALID_LENGTH;  // :180
-                else if (!(lc != kNone && lc < le)) route = SR_ROUTE_INVALID_FORMAT;                                       // :140
-                else route = probe_shard(h, p, bd.probed_dead, lpd);                                                      // :145
-                sr_record r;
-                r.offset = (uint32_t)(T0 + ls);
-                r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
-                r.route = (uint16_t)route;
-                if (!have_base) {   // needed only now, after the hash: normally long published
-                    stamp<ABL>(p, tid, g, 3);
-                    base = granule_ok(st_early, epoch & 0x3FFFFFFFu, kFlagBase)
-                               ? (uint32_t)st_early
-                               : wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
-                    stamp<ABL>(p, tid, g, 7);
-                    have_base = true;
-                }
-                const uint32_t rec = base + (uint32_t)j;
-                if (rec < bd.max_records) {
-                    if (route == kRoutePending) {
-                        const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
-                        if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
-                    }
-                    bd.recs[rec] = r;
-                    if (bd.hashes) bd.hashes[rec] = h;
-                }
-            };
-            // Tile-wide lane groups: every line G lanes, lane gi of the line's Gl lanes takes the
-            // 64-byte segments gi, gi + Gl, ... (a longer line's lanes walk several segments).
+            // One line's work: bounds, verdict, sdbm (lane gi of the line's Gl lanes takes the
+            // 64-byte segments gi, gi + Gl, ...), shard, record. Gw: the wave-uniform bound of
+            // the lane groups (groups are aligned to their size, so xor partners below Gl stay
+            // inside the group).
             auto line = [&](int jj, bool act, int gi, int Gl, int Gw) {
-                int ls, le, lc;
-                geom(jj, act, ls, le, lc);
-                const int len = le - ls + 1;
+                const int j = wbase + jj;
+                const int e = act ? sm.lend[jj + 1] : 0;
+                int c = act ? sm.lcol[jj + 1] : kNone;
+                if (j == 0 && c_pre != kNone) c = c_pre;   // the straddling line's ':' lies before T0
+                const int s = (j == 0) ? s_pre : (act ? sm.lend[jj] + 1 : 0);
+                const int len = e - s + 1;
                 const bool len_ok = len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH;   // :180
-                const bool fmt_ok = lc != kNone && lc < le;                                             // :140
+                const bool fmt_ok = c != kNone && c < e;                                                // :140
                 uint64_t h = 0;
                 if (act && len_ok && fmt_ok && !(ABL & ABL_NO_HASH)) {
                     // sdbm of [s, c) = sum over 64-byte segments k of Horner(seg_k) * K^(c - end_k)
-                    const int n = lc - ls, nseg = (n + 63) >> 6;
+                    const int n = c - s, nseg = (n + 63) >> 6;
                     for (int k = gi; k < nseg; k += Gl) {
-                        const int a = ls + 64 * k, nn = min(64, n - 64 * k);
+                        const int a = s + 64 * k, nn = min(64, n - 64 * k);
                         const bool mid = !(ABL & (ABL_NO_MID_BASE | ABL_EARLY_BASE)) && !have_base && k == gi;
                         uint64_t hs = (ABL & ABL_OLD_HASH) ? sdbm_lds(sm, a + kHalo, nn)
                                                            : sdbm_img(sm, a + kHalo, nn, mid ? base_slot : nullptr, &st_early);
-                        if (k + 1 < nseg) hs *= kpow_n(sm, lc - a - nn);   // the last segment ends at c
+                        if (k + 1 < nseg) hs *= kpow_n(sm, c - a - nn);   // the last segment ends at c
                         h += hs;
                     }
                 }
@@ -1354,115 +1312,137 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     const uint64_t v = shfl_xor64(h, d);
                     if (d < Gl) h += v;
                 }
-                return h;
-            };
-            // Segment map for mixed lengths (single-window tiles, G > 1): lane x of the workgroup
-            // hashes the x-th 64-byte name segment of the window, whichever line it belongs to, so
-            // a 64-byte line takes one lane and a 1024-byte line sixteen (tile-wide groups leave
-            // 7 of a 64-byte line's 8 lanes idle in a C5 tile). Thread tid knows line tid's segment
-            // count and, from a block scan, its first segment; segment starts are bits of an LDS
-            // map, so lane x finds its line by a prefix popcount. The per-segment terms are summed
-            // per line through LDS after a barrier (the image is no longer needed then).
-            bool segmode = false;
-            int my_sf = 0, my_nseg = 0;
-            int rj = -1;        // the window line this thread records, and its name hash
-            uint64_t rh = 0;
-            uint32_t TS = 0;
-            if (G > 1 && !(ABL & (ABL_NO_HASH | ABL_OLD_HASH))) {
-                {
-                    int ls, le, lc;
-                    geom(tid, tid < nwin, ls, le, lc);
-                    const int len = le - ls + 1;
-                    const bool ok = tid < nwin && len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH &&
-                                    lc != kNone && lc < le;
-                    my_nseg = ok ? (lc - ls + 63) >> 6 : 0;
+                if (act && gi == 0) {
+                    uint32_t route;
+                    if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
+                    else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
+                    else route = probe_shard(h, p, bd.probed_dead);                                    // :145
+                    sr_record r;
+                    r.offset = (uint32_t)(T0 + s);
+                    r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
+                    r.route = (uint16_t)route;
+                    if (!have_base) {   // needed only now, after the hash: normally long published
+                        stamp<ABL>(p, tid, g, 3);
+                        base = granule_ok(st_early, epoch & 0x3FFFFFFFu, kFlagBase)
+                                   ? (uint32_t)st_early
+                                   : wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
+                        stamp<ABL>(p, tid, g, 7);
+                        have_base = true;
+                    }
+                    const uint32_t rec = base + (uint32_t)j;
+                    if (rec < bd.max_records) {
+                        if (route == kRoutePending) {
+                            const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
+                            if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
+                        }
+                        bd.recs[rec] = r;
+                        if (bd.hashes) bd.hashes[rec] = h;
+                    }
                 }
-                if (tid < S::kSegWords) sm.segbits[tid] = 0u;
-                const uint32_t incl = wave_incl_add32((uint32_t)my_nseg);
-                const uint32_t wmax = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max32((uint32_t)my_nseg), 63);
-                if (lane == 63) {
-                    sm.segw[wave][0] = incl;
-                    sm.segw[wave][1] = wmax;
+            };
+            // Lane classes: thread tid describes line tid of the window; class k = log2 of the
+            // lanes its hash wants (2^k >= its 64-byte segments, at most 32).
+            int ncl = 0;
+            uint32_t TL = 0, Gmax = 1;   // lanes all lines want; the largest class
+            // only tiles of long lines on average (G > 1) can gain; C2-like tiles skip this
+            const bool classify = (ABL & ABL_MIXED_LANES) && G > 1;
+            if (classify) {
+                if (tid < nwin) {
+                    const int jj = tid, j = wbase + jj;
+                    const int e = sm.lend[jj + 1];
+                    int c = sm.lcol[jj + 1];
+                    if (j == 0 && c_pre != kNone) c = c_pre;
+                    const int s = (j == 0) ? s_pre : sm.lend[jj] + 1;
+                    const int len = e - s + 1;
+                    if (len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH && c != kNone && c < e) {
+                        const int nseg = (c - s + 63) >> 6;
+                        ncl = nseg <= 1 ? 0 : min(5, 32 - __builtin_clz((unsigned)(nseg - 1)));
+                    }
+                }
+                const uint32_t want = tid < nwin ? 1u << ncl : 0u;
+                const uint32_t wsum = wave_add32(want);
+                const uint32_t wmax = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max32(want), 63);
+                if (lane == 0) {
+                    sm.ccnt[wave][0] = wsum;
+                    sm.ccnt[wave][1] = wmax;
                 }
                 wg_barrier();
-                uint32_t before = 0, maxseg = 0;
+                uint32_t cls_or = 0;
 #pragma unroll
                 for (int w = 0; w < kWaves; ++w) {
-                    const uint32_t tw = sm.segw[w][0];
-                    TS += tw;
-                    maxseg = max(maxseg, sm.segw[w][1]);
-                    if (w < wave) before += tw;
+                    TL += sm.ccnt[w][0];
+                    cls_or = max(cls_or, sm.ccnt[w][1]);
                 }
-                TS = __builtin_amdgcn_readfirstlane(TS);
-                maxseg = __builtin_amdgcn_readfirstlane(maxseg);
-                my_sf = (int)(before + incl) - my_nseg;
-                const int cost_tile = ((nwin * G + BLOCK - 1) / BLOCK) * (((int)maxseg + G - 1) / G);
-                const int cost_seg = ((int)TS + BLOCK - 1) / BLOCK + 1;
-                segmode = nwin == (int)tile_count && TS <= (uint32_t)(S::kSegRounds * BLOCK) && cost_seg < cost_tile;
-                if (segmode) {
-                    if (my_nseg) atomicOr(&sm.segbits[my_sf >> 5], 1u << (my_sf & 31));
-                    wg_barrier();
-                    if (wave == 0) {   // lines starting in earlier map words
-                        const uint32_t pc = lane < S::kSegWords ? (uint32_t)__popc(sm.segbits[lane]) : 0u;
-                        const uint32_t inc = wave_incl_add32(pc);
-                        if (lane < S::kSegWords) sm.segpre[lane] = (uint16_t)(inc - pc);
-                    }
-                    wg_barrier();
-                }
+                TL = __builtin_amdgcn_readfirstlane(TL);
+                Gmax = max(1u, (uint32_t)__builtin_amdgcn_readfirstlane(cls_or));
             }
-            if (segmode) {
-                // the record base, requested now; it arrives while the segments are hashed
-                if (!have_base) st_early = __hip_atomic_load(base_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                uint64_t part[S::kSegRounds];
+            // Rounds either way: the tile-wide G (every line G lanes; a longer line's lanes walk
+            // several segments) or one lane group per line sized to the line (groups packed in
+            // descending size). The latter wins on mixed lengths (C5).
+            const int cost_tile = ((nwin * G + BLOCK - 1) / BLOCK) * (((int)Gmax + G - 1) / G);
+            const int cost_mixed = ((int)TL + BLOCK - 1) / BLOCK + 1;
+            const bool mixed = classify && cost_mixed <= cost_tile;
+            if (mixed) {
+                // counting sort of the window's lines by class, largest first, into sm.lorder;
+                // sm.ctab[k] = (first lane of class k << 16) | (first sorted slot of class k)
+                uint32_t rank = 0;
+                wg_barrier();   // every wave has read the totals before ccnt is reused
 #pragma unroll
-                for (int r = 0; r < S::kSegRounds; ++r) {
-                    part[r] = 0;
-                    const int x = r * BLOCK + tid;
-                    if (r * BLOCK < (int)TS && x < (int)TS) {
-                        const int w = x >> 5, bit = x & 31;
-                        const uint32_t below = sm.segbits[w] & (bit == 31 ? 0xFFFFFFFFu : ((2u << bit) - 1u));
-                        const int jj = (int)sm.segpre[w] + __popc(below) - 1;
-                        int xs;   // the line's first segment: the highest map bit at or below x
-                        if (below) {
-                            xs = w * 32 + 31 - __builtin_clz(below);
-                        } else {
-                            int ww = w - 1;
-                            while (sm.segbits[ww] == 0u) --ww;
-                            xs = ww * 32 + 31 - __builtin_clz(sm.segbits[ww]);
-                        }
-                        const int k = x - xs;
-                        int ls, le, lc;
-                        geom(jj, true, ls, le, lc);
-                        const int n = lc - ls, nseg = (n + 63) >> 6;
-                        const int a = ls + 64 * k, nn = min(64, n - 64 * k);
-                        uint64_t hs = sdbm_img(sm, a + kHalo, nn);
-                        if (k + 1 < nseg) hs *= kpow_n(sm, lc - a - nn);
-                        part[r] = hs;
+                for (int k = 0; k < 6; ++k) {
+                    const uint64_t m = __ballot(tid < nwin && ncl == k);
+                    if (lane == 0) sm.ccnt[wave][k] = (uint32_t)__popcll(m);
+                    if (ncl == k) rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+                }
+                wg_barrier();
+                if (tid == 0) {
+                    uint32_t lo = 0, first = 0;
+                    for (int k = 5; k >= 0; --k) {
+                        uint32_t n = 0;
+                        for (int w = 0; w < kWaves; ++w) n += sm.ccnt[w][k];
+                        sm.ctab[k] = (lo << 16) | first;
+                        lo += n << k;
+                        first += n;
                     }
                 }
-                wg_barrier();   // every segment is hashed: the image is free for the terms
-                uint64_t *const terms = reinterpret_cast<uint64_t *>(&sm.img[0]);
-#pragma unroll
-                for (int r = 0; r < S::kSegRounds; ++r)
-                    if (r * BLOCK + tid < (int)TS) terms[r * BLOCK + tid] = part[r];
                 wg_barrier();
                 if (tid < nwin) {
-                    for (int k = 0; k < my_nseg; ++k) rh += terms[my_sf + k];
-                    rj = tid;
+                    uint32_t pos = (sm.ctab[ncl] & 0xFFFFu) + rank;
+                    for (int w = 0; w < wave; ++w) pos += sm.ccnt[w][ncl];
+                    sm.lorder[pos] = (uint8_t)tid;
                 }
-            } else {
-                // one round: nwin * G <= BLOCK (G > 1 only when G * tile_count < BLOCK)
-                const int jj = tid >> __builtin_ctz((unsigned)G), gi = tid & (G - 1);
-                const uint64_t h = line(jj, jj < nwin, gi, G, G);
-                if (jj < nwin && gi == 0) {
-                    rj = jj;
-                    rh = h;
-                }
+                wg_barrier();
             }
-            if (rj >= 0) {
-                int ls, le, lc;
-                geom(rj, true, ls, le, lc);
-                record(rj, ls, le, lc, rh);
+            // wave-uniform rounds over the lanes the lines want (the base resolution needs every
+            // lane of the wave): tile-wide G, or the sorted per-line groups
+            const int lanes_total = mixed ? (int)TL : nwin * G;
+            const int Gw = mixed ? (int)Gmax : G;
+            for (int r0 = 0; r0 < lanes_total; r0 += BLOCK) {
+                const uint32_t x = (uint32_t)(r0 + tid);
+                int jj, gi, Gl;
+                bool act;
+                if (!mixed) {
+                    jj = (int)(x >> __builtin_ctz((unsigned)G));
+                    gi = (int)(x & (uint32_t)(G - 1));
+                    Gl = G;
+                    act = jj < nwin;
+                } else {
+                    // the class whose lane range [lo_k, lo_(k-1)) holds x (class 5 starts at lane 0)
+                    int k = -1;
+#pragma unroll
+                    for (int kk = 5; kk >= 0; --kk) {
+                        const uint32_t lo = sm.ctab[kk] >> 16;
+                        const uint32_t hi = kk ? (sm.ctab[kk - 1] >> 16) : TL;
+                        if (k < 0 && x >= lo && x < hi) k = kk;
+                    }
+                    act = k >= 0;
+                    const int kc = act ? k : 0;
+                    const uint32_t t = sm.ctab[kc];
+                    const uint32_t off = act ? x - (t >> 16) : 0u;
+                    jj = act ? (int)sm.lorder[(t & 0xFFFFu) + (off >> kc)] : 0;
+                    gi = (int)(off & ((1u << kc) - 1u));
+                    Gl = 1 << kc;
+                }
+                line(jj, act, gi, Gl, Gw);
             }
         }
 
@@ -1537,19 +1517,10 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
                                        : __hip_atomic_load(&p.ctl->scan_xcc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < S::kPowWords) ((uint32_t *)&sm.kp_lo[0])[tid] = kp;   // kp_lo | kp_hi | kp_inv are contiguous
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
-    if (tid < (int)(kLdsDeadBits / 32)) sm.pdead[tid] = 0u;   // ordered before any probe by the barriers between
     uint64_t nlm, clm;
     uint32_t c_in;
     tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
     tile_lines<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
-    if (p.dead && p.b[bi].probed_dead && p.nds <= kLdsDeadBits) {   // flush the tile's probed-dead bits
-        wg_barrier();
-        if (tid < (int)((p.nds + 31) / 32)) {
-            const uint32_t v = sm.pdead[tid];
-            if (v) __hip_atomic_fetch_or(reinterpret_cast<uint32_t *>(p.b[bi].probed_dead) + tid, v, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
     if (tid == 0) arrive(p, blockIdx.x, ep0);
     stamp<ABL>(p, tid, g, 9);
 }

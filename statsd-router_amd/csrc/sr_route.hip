@@ -225,18 +225,19 @@ int sr_route_device_many(sr_ctx *c, const sr_batch *batches, size_t count) {
     return 0;
 }
 
-int sr_pack_by_owner(sr_ctx *c, const uint8_t *d_bytes, size_t nbytes, const sr_record *d_recs,
-                     const uint64_t *d_n_records, size_t max_records, uint32_t n_owners, uint8_t *d_out_bytes,
-                     size_t out_cap, sr_record *d_out_recs, uint64_t *d_owner_counts) {
-    if (!c || !d_n_records || !d_owner_counts || n_owners == 0 || n_owners > SR_MAX_OWNERS) return -EINVAL;
-    // the packed layout is addressed with u32 offsets: its worst case must fit 32 bits, and the
-    // caller's buffer must hold that worst case (the kernels never truncate silently)
-    if (max_records > 0xFFFFFFFFull || SR_PACK_CAPACITY((uint64_t)nbytes) > 0xFFFFFFFFull) return -EINVAL;
-    if (out_cap < SR_PACK_CAPACITY((uint64_t)nbytes)) return -EINVAL;
-    if (out_cap > 0xFFFFFFFFull) out_cap = 0xFFFFFFFFull;
-    if (max_records && (!d_recs || !d_out_recs || !d_bytes || !d_out_bytes)) return -EINVAL;
-    (void)hipSetDevice(c->device);
-    const uint32_t ntiles = (uint32_t)((max_records + kPackTile - 1) / kPackTile);
+static int pack_launch(sr_ctx *c, const PackBatch *in, uint32_t nb, uint32_t n_owners, uint8_t *d_out_bytes,
+                       size_t out_cap, sr_record *d_out_recs, uint64_t *d_owner_counts) {
+    PackParams p;
+    memset(&p, 0, sizeof(p));
+    uint32_t ntiles = 0;
+    for (uint32_t j = 0; j < nb; ++j) {
+        p.b[j] = in[j];
+        p.b[j].tile0 = ntiles;
+        ntiles += (in[j].max_records + kPackTile - 1) / kPackTile;
+    }
+    p.nb = nb ? nb : 1;
+    p.n_owners = n_owners;
+    p.ntiles = ntiles;
     const size_t need = (size_t)(ntiles ? ntiles : 1) * n_owners;
     if (need > c->pack_tiles_cap) {
         (void)hipFree(c->d_pack_tiles);
@@ -247,14 +248,6 @@ int sr_pack_by_owner(sr_ctx *c, const uint8_t *d_bytes, size_t nbytes, const sr_
     }
     if (!c->d_owner_start && hipMalloc(&c->d_owner_start, 2 * SR_MAX_OWNERS * sizeof(uint64_t)) != hipSuccess)
         return -ENOMEM;
-    PackParams p;
-    p.bytes = d_bytes;
-    p.nbytes = (uint32_t)nbytes;
-    p.n_owners = n_owners;
-    p.recs = d_recs;
-    p.n_records = d_n_records;
-    p.max_records = (uint32_t)max_records;
-    p.ntiles = ntiles;
     p.tile_counts = c->d_pack_tiles;
     p.tile_base = c->d_pack_tiles + c->pack_tiles_cap;
     p.owner_start = c->d_owner_start;
@@ -273,6 +266,41 @@ int sr_pack_by_owner(sr_ctx *c, const uint8_t *d_bytes, size_t nbytes, const sr_
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
     return 0;
+}
+
+int sr_pack_by_owner(sr_ctx *c, const uint8_t *d_bytes, size_t nbytes, const sr_record *d_recs,
+                     const uint64_t *d_n_records, size_t max_records, uint32_t n_owners, uint8_t *d_out_bytes,
+                     size_t out_cap, sr_record *d_out_recs, uint64_t *d_owner_counts) {
+    if (!c || !d_n_records || !d_owner_counts || n_owners == 0 || n_owners > SR_MAX_OWNERS) return -EINVAL;
+    // the packed layout is addressed with u32 offsets: its worst case must fit 32 bits, and the
+    // caller's buffer must hold that worst case (the kernels never truncate silently)
+    if (max_records > 0xFFFFFFFFull || SR_PACK_CAPACITY((uint64_t)nbytes) > 0xFFFFFFFFull) return -EINVAL;
+    if (out_cap < SR_PACK_CAPACITY((uint64_t)nbytes)) return -EINVAL;
+    if (out_cap > 0xFFFFFFFFull) out_cap = 0xFFFFFFFFull;
+    if (max_records && (!d_recs || !d_out_recs || !d_bytes || !d_out_bytes)) return -EINVAL;
+    (void)hipSetDevice(c->device);
+    PackBatch b{d_bytes, d_recs, d_n_records, (uint32_t)nbytes, (uint32_t)max_records, 0, 0};
+    return pack_launch(c, &b, 1, n_owners, d_out_bytes, out_cap, d_out_recs, d_owner_counts);
+}
+
+int sr_pack_many_by_owner(sr_ctx *c, const sr_batch *batches, size_t count, uint32_t n_owners, uint8_t *d_out_bytes,
+                          size_t out_cap, sr_record *d_out_recs, uint64_t *d_owner_counts) {
+    if (!c || !d_owner_counts || n_owners == 0 || n_owners > SR_MAX_OWNERS) return -EINVAL;
+    if (count == 0 || count > SR_MAX_BATCHES_PER_LAUNCH || !batches) return -EINVAL;
+    uint64_t total_bytes = 0;
+    PackBatch in[kPackMaxBatches];
+    for (size_t j = 0; j < count; ++j) {
+        const sr_batch &b = batches[j];
+        if (!b.d_n_records || b.max_records > 0xFFFFFFFFull || b.nbytes > 0xFFFFFFF0ull) return -EINVAL;
+        if (b.max_records && (!b.d_out || !b.d_bytes)) return -EINVAL;
+        total_bytes += b.nbytes;
+        in[j] = PackBatch{b.d_bytes, b.d_out, b.d_n_records, (uint32_t)b.nbytes, (uint32_t)b.max_records, 0, 0};
+    }
+    if (SR_PACK_CAPACITY(total_bytes) > 0xFFFFFFFFull || out_cap < SR_PACK_CAPACITY(total_bytes)) return -EINVAL;
+    if (out_cap > 0xFFFFFFFFull) out_cap = 0xFFFFFFFFull;
+    if (!d_out_bytes || !d_out_recs) return -EINVAL;
+    (void)hipSetDevice(c->device);
+    return pack_launch(c, in, (uint32_t)count, n_owners, d_out_bytes, out_cap, d_out_recs, d_owner_counts);
 }
 
 // Scratch of the packing kernels for max_records records (grown, never shrunk; not in capture).

@@ -144,3 +144,38 @@ class Regrouper:
     def __call__(self, d_bytes: int, nbytes: int, d_recs: int, d_n_records: int, max_records: int):
         self.pack(d_bytes, nbytes, d_recs, d_n_records, max_records)
         return self.exchange()
+
+
+class LaunchRegrouper:
+    """Pack + exchange of a whole route launch (up to SR_MAX_BATCHES_PER_LAUNCH batches) at once:
+    one sr_pack_many_by_owner (owner chunks hold batch 0's lines, then batch 1's, ...), one
+    all-to-all of the split sizes with one host round trip, then the packed lines and the records
+    (RCCL over xGMI with the "nccl" backend; gloo in the CPU tests). Same stream rule as Regrouper."""
+
+    def __init__(self, pkg, router, max_total_bytes: int, max_total_records: int, group=None):
+        self.pkg, self.router, self.group = pkg, router, group
+        self.G = dist.get_world_size(group)
+        if not 1 <= self.G <= pkg.SR_MAX_OWNERS:
+            raise ValueError(f"regroup over {self.G} ranks: at most {pkg.SR_MAX_OWNERS}")
+        dev = torch.device("cuda", router.device)
+        self.cap = pkg.pack_capacity(max_total_bytes)
+        self.max_records = max_total_records
+        self.bytes = torch.empty(self.cap, dtype=torch.uint8, device=dev)
+        self.recs = torch.empty(max(max_total_records, 1), dtype=torch.int64, device=dev)
+        self.counts = torch.zeros((self.G, 2), dtype=torch.int64, device=dev)
+        self.last_sent: list = []
+        self.last_received: list = []
+
+    def __call__(self, batches):
+        """batches = [(d_bytes, nbytes, d_recs, max_records, d_n_records), ...] routed on the router's
+        stream. Returns (recv_bytes, recv_recs (offsets into recv_bytes), recv_counts [G, 2])."""
+        h = getattr(self.router, "stream_handle", 0)
+        if h == 0 or h != torch.cuda.current_stream().cuda_stream:
+            raise RuntimeError("LaunchRegrouper: router.set_stream(s.cuda_stream) with s = torch's current stream "
+                               "(a non-default stream) is required")
+        if sum(b[3] for b in batches) > self.max_records or self.pkg.pack_capacity(sum(b[1] for b in batches)) > self.cap:
+            raise ValueError("launch larger than the regrouper's buffers")
+        self.router.pack_many_by_owner(batches, self.G, self.bytes.data_ptr(), self.cap, self.recs.data_ptr(),
+                                       self.counts.data_ptr())
+        rb, rr, rc, self.last_sent, self.last_received = _exchange(self.bytes, self.recs, self.counts, self.group)
+        return rb, rr, rc

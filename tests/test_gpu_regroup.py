@@ -107,3 +107,38 @@ def test_regrouper_two_slots_pipelined(pkg, oracle, torch_stream):
                 assert rc.tolist() == ec.tolist()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("G,n_shards,nb", [(1, 4, 3), (3, 16, 5), (8, 64, 8), (64, 100, 2)])
+def test_pack_many_by_owner_matches_oracle(pkg, oracle, G, n_shards, nb, torch_stream):
+    """sr_pack_many_by_owner over a launch's batches = the per-batch packs concatenated per owner."""
+    import torch
+
+    streams = [pkg.gen_stream(1 << 18, [64, 256, 1024], seed=900 + 7 * G + b, p_invalid=0.05) for b in range(nb)]
+    alive = [int(k % 5 != 1) for k in range(n_shards)]
+    cap = max(s.n_lines for s in streams)
+    d_in = torch.zeros((nb, 1 << 18), dtype=torch.uint8, device="cuda")
+    for b, s in enumerate(streams):
+        d_in[b, : s.data.size].copy_(torch.from_numpy(s.data))
+    d_rec = torch.zeros((nb, cap), dtype=torch.int64, device="cuda")
+    d_n = torch.zeros(nb, dtype=torch.int64, device="cuda")
+    total = sum(int(s.data.size) for s in streams)
+    out_cap = pkg.pack_capacity(total)
+    d_pb = torch.full((out_cap,), 0xAB, dtype=torch.uint8, device="cuda")
+    d_pr = torch.zeros(nb * cap, dtype=torch.int64, device="cuda")
+    d_cnt = torch.zeros((G, 2), dtype=torch.int64, device="cuda")
+    with pkg.Router(n_shards, 1 << 18) as r:
+        r.set_alive(alive)
+        r.set_stream(torch_stream.cuda_stream)
+        r.route_device_many([(d_in[b].data_ptr(), int(s.data.size), d_rec[b].data_ptr(), cap, None, d_n[b].data_ptr())
+                             for b, s in enumerate(streams)])
+        r.pack_many_by_owner([(d_in[b].data_ptr(), int(s.data.size), d_rec[b].data_ptr(), cap, d_n[b].data_ptr())
+                              for b, s in enumerate(streams)], G, d_pb.data_ptr(), out_cap, d_pr.data_ptr(),
+                             d_cnt.data_ptr())
+        torch.cuda.synchronize()
+    recs_list = [oracle.route(s.data, n_shards, alive)[0] for s in streams]
+    eb, er, ec = oracle.pack_many_by_owner([s.data for s in streams], recs_list, G)
+    assert d_cnt.cpu().numpy().tolist() == ec.tolist()
+    assert np.array_equal(d_pb[: eb.size].cpu().numpy(), eb)
+    got = np.frombuffer(d_pr[: len(er)].cpu().numpy().tobytes(), dtype=pkg.RECORD_DTYPE)
+    assert np.array_equal(got, er)

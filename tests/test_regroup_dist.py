@@ -25,16 +25,17 @@ def _free_port():
     return p
 
 
-def _inputs(pkg, oracle, rank, n_shards, alive):
+def _inputs(pkg, oracle, rank, n_shards, alive, b=0):
     if rank == 2:   # a rank with nothing valid to send
         data = np.frombuffer(pkg.frame_datagrams([b"no colon here\n", b"x\n", b"AAAA" * 400]), dtype=np.uint8)
     else:
-        data = pkg.gen_stream(150_000 + 50_000 * rank, [64, 256, 1024], seed=77 + rank, p_invalid=0.1).data
+        data = pkg.gen_stream(150_000 + 50_000 * rank - 20_000 * b, [64, 256, 1024], seed=77 + rank + 100 * b,
+                              p_invalid=0.1).data
     recs, _, n = oracle.route(data, n_shards, alive)
     return data, recs
 
 
-def _worker(rank, world, port, n_shards, q):
+def _worker(rank, world, port, n_shards, q, nb=1):
     try:
         sys.path.insert(0, REPO)
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -48,19 +49,23 @@ def _worker(rank, world, port, n_shards, q):
         import sr_oracle as oracle
 
         alive = [0 if k % 7 == 3 else 1 for k in range(n_shards)]
-        data, recs = _inputs(pkg, oracle, rank, n_shards, alive)
-        pb, pr, cnt = oracle.pack_by_owner(data, recs, world)
+        ins = [_inputs(pkg, oracle, rank, n_shards, alive, b) for b in range(nb)]
+        if nb == 1:
+            pb, pr, cnt = oracle.pack_by_owner(ins[0][0], ins[0][1], world)
+        else:   # a launch's batches packed together (sr_pack_many_by_owner's layout)
+            pb, pr, cnt = oracle.pack_many_by_owner([d for d, _ in ins], [r for _, r in ins], world)
         rb, rr, rc = rg.exchange_packed(torch.from_numpy(pb), torch.from_numpy(pr.view(np.int64)),
                                         torch.from_numpy(cnt), None)
         rb, rr = rb.numpy(), rr.numpy().view(pkg.RECORD_DTYPE)
         # expected: every source's valid lines of the shards this rank owns, source by source
         exp_lines, exp_routes = [], []
         for s in range(world):
-            d, r = _inputs(pkg, oracle, s, n_shards, alive)
-            for x in r:
-                if x["route"] < 0xFFFD and x["route"] % world == rank:
-                    exp_lines.append(bytes(d[x["offset"]: x["offset"] + x["length"]]))
-                    exp_routes.append(int(x["route"]))
+            for b in range(nb):
+                d, r = _inputs(pkg, oracle, s, n_shards, alive, b)
+                for x in r:
+                    if x["route"] < 0xFFFD and x["route"] % world == rank:
+                        exp_lines.append(bytes(d[x["offset"]: x["offset"] + x["length"]]))
+                        exp_routes.append(int(x["route"]))
         assert len(rr) == len(exp_lines), (len(rr), len(exp_lines))
         got = [bytes(rb[x["offset"]: x["offset"] + x["length"]]) for x in rr]
         assert got == exp_lines
@@ -73,12 +78,12 @@ def _worker(rank, world, port, n_shards, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world,n_shards", [(2, 64), (3, 16), (2, 1)])
-def test_regroup_exchange_gloo(world, n_shards):
+@pytest.mark.parametrize("world,n_shards,nb", [(2, 64, 1), (3, 16, 1), (2, 1, 1), (2, 64, 3), (3, 16, 2)])
+def test_regroup_exchange_gloo(world, n_shards, nb):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_shards, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_shards, q, nb)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
