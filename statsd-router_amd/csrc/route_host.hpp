@@ -208,6 +208,7 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
     }
     RouteParams p = in;
     p.nb = 0;
+    uint64_t replay_blocks = 0;   // probed_dead_kernel blocks (batches that asked for the bitmap)
     for (uint32_t i = 0; i < in.nb; ++i) {
         // the probed-dead bitmap starts empty; with every shard alive nothing can set it
         if (in.b[i].probed_dead) {
@@ -223,6 +224,7 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
         }
         p.b[p.nb++] = in.b[i];
         if (ds.dead == 0) p.b[p.nb - 1].probed_dead = nullptr;
+        if (p.b[p.nb - 1].probed_dead) replay_blocks += (p.b[p.nb - 1].max_records + 255u) / 256u;
     }
     if (p.nb == 0) return 0;
     // 8+ batches: each batch's tiles on one XCD class; its scanner (block j) shares that class
@@ -268,6 +270,11 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
             attr_set = true;
         }
         hipLaunchKernelGGL(probe_wide_kernel, dim3(256), dim3(64), (size_t)ds.nds * sizeof(uint16_t), stream, p);
+        if (hipGetLastError() != hipSuccess) return -EIO;
+    }
+    if (replay_blocks) {   // dead shards and a bitmap asked for: replay the probes (sr-main.c:106)
+        if (replay_blocks > 0x7FFFFFFFull) return -EINVAL;
+        hipLaunchKernelGGL(probed_dead_kernel, dim3((uint32_t)replay_blocks), dim3(256), 0, stream, p);
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
     return 0;

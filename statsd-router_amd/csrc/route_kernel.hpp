@@ -488,12 +488,15 @@ __device__ __noinline__ void note_all_dead(uint64_t *pd, uint32_t n) {
 }
 
 // find_downstream (sr-main.c:86-117) for one line. Returns the shard, SR_ROUTE_ALL_DEAD, or
-// kRoutePending if more than kOverlay dead shards had to be probed. pd (may be null): the batch's
-// probed-dead bitmap.
-__device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *pd) {
+// kRoutePending if more than kOverlay dead shards had to be probed. The dead shards the probe
+// visits (sr-main.c:106) are recorded by probed_dead_kernel, a replay after the launch: any extra
+// live value in this loop costs the route kernel a spill (measured: 9 % at C2, all alive).
+// MARK: when non-null, every dead shard visited is set in that bitmap (the replay's use).
+template <bool MARK = false>
+__device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark = nullptr) {
     const uint32_t n = p.nds;
     if (p.dead >= n) {                                    // includes N == 0
-        if (pd && n) note_all_dead(pd, n);
+        if (MARK && n) note_all_dead(mark, n);
         return SR_ROUTE_ALL_DEAD;
     }
     if (p.dead == 0) return mod_magic(h, p.magic_n, n);   // every shard alive: j = h % N
@@ -510,7 +513,7 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *pd) 
         for (int e = 0; e < kOverlay; ++e)
             if ((ov[e] >> 16) == j) k = ov[e] & 0xFFFFu;
         if (alive_bit(p.alive, k)) return k;                         // :101-104
-        if (pd) note_dead(pd, k);                                    // :106
+        if (MARK) note_dead(mark, k);                                // :106
         if (j != i - 1) {                                            // :108-111
             uint32_t v = i - 1;
 #pragma unroll
@@ -1316,7 +1319,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     uint32_t route;
                     if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
                     else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
-                    else route = probe_shard(h, p, bd.probed_dead);                                    // :145
+                    else route = probe_shard(h, p);                                                    // :145
                     sr_record r;
                     r.offset = (uint32_t)(T0 + s);
                     r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
@@ -1562,6 +1565,53 @@ __global__ __launch_bounds__(64) void probe_wide_kernel(RouteParams p) {
             h = (h * 7 + 5) / 3;
         }
     }
+}
+
+// The dead-downstream side effect (sr-main.c:106), replayed after a launch when some shards are
+// dead and a batch asked for its probed-dead bitmap: one lane per record, the name's sdbm
+// recomputed from the batch bytes (aligned dword loads, the first ':' ends it), then the probe of
+// find_downstream with every dead shard it visits set in the bitmap. Lines that needed more than
+// kOverlay dead probes were resolved by probe_wide_kernel, which sets their bits itself.
+__global__ __launch_bounds__(256) void probed_dead_kernel(RouteParams p) {
+    // the batch of this block: batches in order, ceil(max_records / 256) blocks each
+    uint32_t bi = 0, blk = blockIdx.x;
+    for (; bi < p.nb; ++bi) {
+        const uint32_t nbk = (p.b[bi].max_records + 255u) / 256u;
+        if (blk < nbk) break;
+        blk -= nbk;
+    }
+    if (bi >= p.nb) return;
+    const BatchDesc &bd = p.b[bi];
+    if (!bd.probed_dead) return;
+    const uint32_t n = (uint32_t)min(*bd.n_out, (uint64_t)bd.max_records);
+    const uint32_t i = blk * 256u + threadIdx.x;
+    if (i >= n) return;
+    const sr_record r = bd.recs[i];
+    if (r.route == SR_ROUTE_INVALID_LENGTH || r.route == SR_ROUTE_INVALID_FORMAT) return;
+    if (r.route == SR_ROUTE_ALL_DEAD) {   // every shard dead: the probe visited all of them
+        if (p.dead >= p.nds && p.nds) note_all_dead(bd.probed_dead, p.nds);
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
+    // sdbm over the bytes before the first ':' (sr-main.c:120-134); the record is valid, so a ':'
+    // lies within the line
+    uint64_t h = 0;
+    const uint32_t a0 = r.offset & ~3u, end = r.offset + r.length;
+    bool done = false;
+    for (uint32_t a = a0; a < end && !done; a += 4) {
+        const uint32_t x = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t pos = a + (uint32_t)q;
+            const uint32_t c = (x >> (8 * q)) & 0xFFu;
+            if (!done && pos >= r.offset && pos < end) {
+                if (c == (uint32_t)':') done = true;
+                else h = sdbm_step(h, c);
+            }
+        }
+    }
+    (void)probe_shard<true>(h, p, bd.probed_dead);
 }
 
 }  // namespace srk
