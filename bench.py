@@ -75,6 +75,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-pack", action="store_true", help="skip the route + MTU packing leg")
     ap.add_argument("--dry-ranks", action="store_true",
                     help="each rank prints its RANK / LOCAL_RANK / WORLD_SIZE and exits (launcher test; no GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
@@ -303,6 +304,8 @@ def main(argv=None):
             result["cpu_baseline"] = cpu_baseline(host, shards, alive, args.cpu_seconds)
         if not args.no_e2e:
             result["e2e"] = e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M)
+        if not args.no_pack:
+            result["route_pack"] = pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev)
     router.close()
     del d_in, d_out
     torch.cuda.empty_cache()
@@ -487,6 +490,64 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8):
             "note": (f"route launch of {nb} x 16 MiB batches + one sr_pack_many_by_owner + one exchange (split sizes, "
                      f"packed lines, records) per step over {world} GPU(s); owner = shard % {world}; one host round "
                      f"trip per step for the split sizes")}
+
+
+def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev, reps=20):
+    """The router's device data path: one route launch over M batches, then the
+    per-downstream MTU packing of every batch (sr_pack_packets: sorted records + packet
+    descriptors, pending bytes chained batch to batch on the device), captured in one graph and
+    replayed back to back. Reported: lines/s through route + packing, and the packing's own time."""
+    import torch
+
+    max_lines = max(lines)
+    d_rec = torch.empty((M, max_lines), dtype=torch.int64, device=dev)
+    d_cnt = torch.zeros(M, dtype=torch.int64, device=dev)
+    mp = pkg.max_packets(batch_bytes, shards)
+    d_srt = torch.empty((M, max_lines), dtype=torch.int64, device=dev)
+    d_pk = torch.empty((M, mp * 2), dtype=torch.int64, device=dev)
+    d_counts = torch.zeros((M, 3), dtype=torch.int64, device=dev)
+    d_fill = torch.zeros((M + 1, shards), dtype=torch.int16, device=dev)
+    base = d_in.data_ptr()
+
+    def route():
+        router.route_device_many([(base + b * batch_bytes, sizes[b], d_rec[b].data_ptr(), max_lines, None,
+                                   d_cnt[b].data_ptr()) for b in range(M)])
+
+    def pack():
+        for b in range(M):
+            router.pack_packets(d_rec[b].data_ptr(), d_cnt[b].data_ptr(), max_lines, d_fill[b].data_ptr(), None,
+                                d_srt[b].data_ptr(), d_pk[b].data_ptr(), mp, d_counts[b].data_ptr(),
+                                d_fill[b + 1].data_ptr())
+
+    with torch.cuda.stream(stream):
+        route()
+        pack()                                  # eager once: the packing scratch is allocated here
+        stream.synchronize()
+        g_all, g_route = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_all, stream=stream):
+            route()
+            pack()
+        with torch.cuda.graph(g_route, stream=stream):
+            route()
+        res = {}
+        for name, g in (("route_pack", g_all), ("route_only", g_route)):
+            for _ in range(3):
+                g.replay()
+            a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(stream)
+            for _ in range(reps):
+                g.replay()
+            z.record(stream)
+            z.synchronize()
+            res[name] = a.elapsed_time(z) / reps
+    packets = int(d_counts[:, 0].sum())
+    tot_lines = sum(lines[:M])
+    return {"value": round(tot_lines / (res["route_pack"] * 1e-3) / 1e6, 3), "unit": "M metrics/s",
+            "ms_per_launch": round(res["route_pack"], 4), "route_only_ms": round(res["route_only"], 4),
+            "packing_ms": round(res["route_pack"] - res["route_only"], 4),
+            "packets_per_launch": packets,
+            "note": (f"one route launch over {M} batches + sr_pack_packets per batch (regroup by downstream, "
+                     f"next-fit 1450-byte packets, pending bytes chained on the device), one graph, {reps} replays")}
 
 
 def e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M, groups=24):
