@@ -493,10 +493,11 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8):
 
 
 def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev, reps=20):
-    """The router's device data path: one route launch over M batches, then the
-    per-downstream MTU packing of every batch (sr_pack_packets: sorted records + packet
-    descriptors, pending bytes chained batch to batch on the device), captured in one graph and
-    replayed back to back. Reported: lines/s through route + packing, and the packing's own time."""
+    """The router's device data path: one route launch over M batches (the
+    batches of M data threads), then the per-downstream MTU packing of all of them in one
+    sr_pack_packets_many (sorted records + packet descriptors, each batch from its own pending
+    bytes), captured in one graph and replayed back to back. Reported: lines/s through route +
+    packing, and the packing's own time."""
     import torch
 
     max_lines = max(lines)
@@ -506,18 +507,18 @@ def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, de
     d_srt = torch.empty((M, max_lines), dtype=torch.int64, device=dev)
     d_pk = torch.empty((M, mp * 2), dtype=torch.int64, device=dev)
     d_counts = torch.zeros((M, 3), dtype=torch.int64, device=dev)
-    d_fill = torch.zeros((M + 1, shards), dtype=torch.int16, device=dev)
+    d_fill = torch.zeros((M, shards), dtype=torch.int16, device=dev)
+    d_fout = torch.zeros((M, shards), dtype=torch.int16, device=dev)
     base = d_in.data_ptr()
 
     def route():
         router.route_device_many([(base + b * batch_bytes, sizes[b], d_rec[b].data_ptr(), max_lines, None,
                                    d_cnt[b].data_ptr()) for b in range(M)])
 
-    def pack():
-        for b in range(M):
-            router.pack_packets(d_rec[b].data_ptr(), d_cnt[b].data_ptr(), max_lines, d_fill[b].data_ptr(), None,
-                                d_srt[b].data_ptr(), d_pk[b].data_ptr(), mp, d_counts[b].data_ptr(),
-                                d_fill[b + 1].data_ptr())
+    def pack():   # the batches of M data threads: independent pending bytes, one set of launches
+        router.pack_packets_many([(d_rec[b].data_ptr(), d_cnt[b].data_ptr(), max_lines, d_fill[b].data_ptr(), 0,
+                                   d_srt[b].data_ptr(), d_pk[b].data_ptr(), mp, d_counts[b].data_ptr(),
+                                   d_fout[b].data_ptr()) for b in range(M)])
 
     with torch.cuda.stream(stream):
         route()
@@ -546,8 +547,8 @@ def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, de
             "ms_per_launch": round(res["route_pack"], 4), "route_only_ms": round(res["route_only"], 4),
             "packing_ms": round(res["route_pack"] - res["route_only"], 4),
             "packets_per_launch": packets,
-            "note": (f"one route launch over {M} batches + sr_pack_packets per batch (regroup by downstream, "
-                     f"next-fit 1450-byte packets, pending bytes chained on the device), one graph, {reps} replays")}
+            "note": (f"one route launch over {M} batches + one sr_pack_packets_many over them (regroup by downstream, "
+                     f"next-fit 1450-byte packets), one graph, {reps} replays")}
 
 
 def e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M, groups=24):

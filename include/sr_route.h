@@ -206,6 +206,23 @@ int sr_pack_packets(sr_ctx *ctx, const sr_record *d_recs, const uint64_t *d_n_re
                     const uint16_t *d_fill_in, const uint64_t *d_probed_dead, sr_record *d_sorted,
                     sr_packet *d_packets, size_t max_packets, uint64_t *d_counts, uint16_t *d_fill_out);
 
+/* Several batches packed in one set of launches (the batches of several data threads, each with
+ * its own pending bytes: batches are independent). Fields as in sr_pack_packets. count <=
+ * SR_MAX_BATCHES_PER_LAUNCH. Same allocation rule as sr_pack_packets. */
+typedef struct sr_pack_batch {
+    const sr_record *d_recs;         /* routed records and their count (sr_route_device(_many))   */
+    const uint64_t *d_n_records;
+    size_t max_records;
+    const uint16_t *d_fill_in;       /* NULL or n_downstreams u16                                 */
+    const uint64_t *d_probed_dead;   /* NULL or the batch's probed-dead bitmap                    */
+    sr_record *d_sorted;
+    sr_packet *d_packets;
+    size_t max_packets;
+    uint64_t *d_counts;              /* 3 u64: {descriptors, valid lines, lines}                  */
+    uint16_t *d_fill_out;
+} sr_pack_batch;
+int sr_pack_packets_many(sr_ctx *ctx, const sr_pack_batch *batches, size_t count);
+
 /* Host-memory batch, routed and packed in one call (what a data thread's read callback needs):
  * `fill` (n_downstreams u16) is the pending bytes per downstream before the batch and receives the
  * pending bytes after it; `sorted` (max_records) the regrouped records; `packets` (max_packets) the

@@ -48,7 +48,7 @@ assert RECORD_DTYPE.itemsize == 8
 ABI_FUNCTIONS = (
     "sr_frame_datagram", "sr_frame_datagrams", "sr_open", "sr_set_alive", "sr_set_stream",
     "sr_route_batch", "sr_last_probed_dead", "sr_route_device", "sr_route_device_many", "sr_pack_by_owner",
-    "sr_pack_many_by_owner", "sr_pack_packets", "sr_route_pack_batch", "sr_alloc_host", "sr_free_host", "sr_sync", "sr_close", "sr_version",
+    "sr_pack_many_by_owner", "sr_pack_packets", "sr_pack_packets_many", "sr_route_pack_batch", "sr_alloc_host", "sr_free_host", "sr_sync", "sr_close", "sr_version",
 )
 SR_MAX_PACK_DOWNSTREAMS = 4096
 PACKET_DTYPE = np.dtype([("first", "<u4"), ("nlines", "<u2"), ("shard", "<u2"), ("length", "<u2"),
@@ -74,6 +74,16 @@ class SrBatch(ctypes.Structure):
         ("d_bytes", ctypes.c_void_p), ("nbytes", ctypes.c_size_t), ("d_out", ctypes.c_void_p),
         ("max_records", ctypes.c_size_t), ("d_hashes", ctypes.c_void_p), ("d_n_records", ctypes.c_void_p),
         ("d_probed_dead", ctypes.c_void_p),
+    ]
+
+
+class SrPackBatch(ctypes.Structure):
+    """struct sr_pack_batch (include/sr_route.h): one batch of sr_pack_packets_many."""
+    _fields_ = [
+        ("d_recs", ctypes.c_void_p), ("d_n_records", ctypes.c_void_p), ("max_records", ctypes.c_size_t),
+        ("d_fill_in", ctypes.c_void_p), ("d_probed_dead", ctypes.c_void_p), ("d_sorted", ctypes.c_void_p),
+        ("d_packets", ctypes.c_void_p), ("max_packets", ctypes.c_size_t), ("d_counts", ctypes.c_void_p),
+        ("d_fill_out", ctypes.c_void_p),
     ]
 
 
@@ -128,6 +138,7 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_pack_many_by_owner": (ctypes.c_int, [vp, ctypes.POINTER(SrBatch), ctypes.c_size_t, ctypes.c_uint32, vp,
                                                  ctypes.c_size_t, vp, vp]),
         "sr_pack_packets": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp, vp, vp, vp, ctypes.c_size_t, vp, vp]),
+        "sr_pack_packets_many": (ctypes.c_int, [vp, ctypes.POINTER(SrPackBatch), ctypes.c_size_t]),
         "sr_route_pack_batch": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, c_size_p, c_size_p,
                                                vp, ctypes.c_size_t, c_size_p, vp]),
         "sr_alloc_host": (vp, [ctypes.c_size_t]),
@@ -361,6 +372,14 @@ class Router:
         vp = ctypes.c_void_p
         _check(self._lib.sr_pack_many_by_owner(self._h, arr, len(batches), n_owners, vp(d_out_bytes), out_cap,
                                                vp(d_out_recs), vp(d_owner_counts)), "sr_pack_many_by_owner")
+
+    def pack_packets_many(self, batches) -> None:
+        """sr_pack_packets_many: batches = [(d_recs, d_n_records, max_records, d_fill_in, d_probed_dead,
+        d_sorted, d_packets, max_packets, d_counts, d_fill_out), ...] (raw device pointers, 0 = NULL)."""
+        arr = (SrPackBatch * max(len(batches), 1))()
+        for i, b in enumerate(batches):
+            arr[i] = SrPackBatch(*[x or None if j not in (2, 7) else x for j, x in enumerate(b)])
+        _check(self._lib.sr_pack_packets_many(self._h, arr, len(batches)), "sr_pack_packets_many")
 
     def sync(self) -> None:
         _check(self._lib.sr_sync(self._h), "sr_sync")

@@ -48,29 +48,100 @@ constexpr int kMtuX = kMtuCap + 1;               // incoming fills 0..1450
 constexpr uint32_t kMtuNone = 0xFFFFFFFFu;
 constexpr uint16_t kMtuEnd = 0xFFFFu;
 
+constexpr int kMtuMaxBatches = 32;
+
+// One batch of a packing launch (user buffers). Batches are independent: each has its own pending
+// bytes in and out (the downstream arrays of different data threads).
+struct MtuBatchArg {
+    const sr_record *recs;
+    const uint64_t *n_records;
+    const uint16_t *fill_in;       // [nds] pending bytes per shard before the batch (null = none)
+    const uint64_t *probed_dead;   // null, or the batch's probed-dead bitmap (route kernel)
+    sr_record *sorted;
+    sr_packet *packets;
+    uint64_t *counts;              // [0] packets, [1] valid lines, [2] lines
+    uint16_t *fill_out;            // [nds]
+    uint32_t max_records;
+    uint32_t max_packets;
+    uint32_t tile0;                // first record tile of the batch in the launch's scratch
+    uint32_t chunk0;               // first chunk of the batch in the launch's scratch
+};
+
+struct MtuLaunch {
+    uint32_t nds, nb, tiles, chunks;   // shards; batches; record tiles and chunks of all batches
+    uint32_t *tile_counts;             // batch b at (nds + 1) * tile0: [(nds + 1) * ntiles], key-major
+    uint32_t *keys;                    // [nb][2 * nds + 4]: key starts (nds + 2) | chunk firsts (nds + 1)
+    uint32_t *chunk_shard;             // [chunks]
+    uint32_t *chunk_entry;             // [chunks] incoming fill
+    uint32_t *chunk_open;              // [chunks] sorted position where the incoming packet began
+    uint32_t *chunk_pk;                // [chunks] first descriptor the chunk writes
+    uint32_t *closed;                  // [nb][nds] packets closed per shard
+    uint64_t *table;                   // [chunks][kMtuX]
+    MtuBatchArg b[kMtuMaxBatches];
+};
+static_assert(sizeof(MtuLaunch) < 3584, "kernel argument size");
+
+// One batch's view of the launch (what the kernels below index).
 struct MtuParams {
     const sr_record *recs;
     const uint64_t *n_records;
     uint32_t max_records;
     uint32_t nds;             // shards; key nds = unrouted lines
-    uint32_t ntiles;          // record tiles (capacity)
-    uint32_t max_chunks;      // chunk capacity
-    const uint16_t *fill_in;  // [nds] pending bytes per shard before the batch (null = none)
-    const uint64_t *probed_dead;   // null, or the batch's probed-dead bitmap (route kernel)
+    uint32_t ntiles;          // record tiles of the batch
+    uint32_t max_chunks;      // chunks of the batch
+    const uint16_t *fill_in;
+    const uint64_t *probed_dead;
     uint32_t *tile_counts;    // [(nds + 1) * ntiles], key-major; scanned in place
     uint32_t *key_start;      // [nds + 2]: first sorted position of each key, [nds + 1] = lines
     uint32_t *chunk_first;    // [nds + 1]: first chunk of each shard, [nds] = chunks
-    uint32_t *chunk_shard;    // [max_chunks]
-    uint64_t *table;          // [max_chunks][kMtuX]
-    uint32_t *chunk_entry;    // [max_chunks] incoming fill
-    uint32_t *chunk_open;     // [max_chunks] sorted position where the incoming packet began (kMtuNone: before the batch)
-    uint32_t *chunk_pk;       // [max_chunks] first descriptor the chunk writes
+    uint32_t *chunk_shard;
+    uint64_t *table;
+    uint32_t *chunk_entry;
+    uint32_t *chunk_open;     // kMtuNone: the incoming packet began before the batch
+    uint32_t *chunk_pk;
+    uint32_t *closed;
     sr_record *sorted;
     sr_packet *packets;
     uint64_t max_packets;
-    uint64_t *counts;         // [0] packets, [1] valid lines, [2] lines
-    uint16_t *fill_out;       // [nds]
+    uint64_t *counts;
+    uint16_t *fill_out;
 };
+
+__device__ __forceinline__ MtuParams mtu_view(const MtuLaunch &L, uint32_t bi) {
+    const MtuBatchArg &a = L.b[bi];
+    MtuParams p;
+    p.recs = a.recs;
+    p.n_records = a.n_records;
+    p.max_records = a.max_records;
+    p.nds = L.nds;
+    p.ntiles = (bi + 1 < L.nb ? L.b[bi + 1].tile0 : L.tiles) - a.tile0;
+    p.max_chunks = (bi + 1 < L.nb ? L.b[bi + 1].chunk0 : L.chunks) - a.chunk0;
+    p.fill_in = a.fill_in;
+    p.probed_dead = a.probed_dead;
+    p.tile_counts = L.tile_counts + (size_t)(L.nds + 1) * a.tile0;
+    p.key_start = L.keys + (size_t)bi * (2 * L.nds + 4);
+    p.chunk_first = p.key_start + L.nds + 2;
+    p.chunk_shard = L.chunk_shard + a.chunk0;
+    p.table = L.table + (size_t)a.chunk0 * kMtuX;
+    p.chunk_entry = L.chunk_entry + a.chunk0;
+    p.chunk_open = L.chunk_open + a.chunk0;
+    p.chunk_pk = L.chunk_pk + a.chunk0;
+    p.closed = L.closed + (size_t)bi * L.nds;
+    p.sorted = a.sorted;
+    p.packets = a.packets;
+    p.max_packets = a.max_packets;
+    p.counts = a.counts;
+    p.fill_out = a.fill_out;
+    return p;
+}
+
+// the batch owning global index g of a per-batch sequence starting at field `first` (nb <= 32)
+template <class F>
+__device__ __forceinline__ uint32_t mtu_batch_of(const MtuLaunch &L, uint32_t g, F first) {
+    uint32_t k = 0;
+    for (uint32_t j = 1; j < L.nb; ++j) k += g >= first(L.b[j]) ? 1u : 0u;
+    return k;
+}
 
 __device__ __forceinline__ uint32_t mtu_lines(const MtuParams &p) {
     return (uint32_t)min(*p.n_records, (uint64_t)p.max_records);
@@ -85,10 +156,12 @@ __device__ __forceinline__ bool mtu_dropped(const MtuParams &p, uint32_t s) {
 }
 
 // ---- sort: histogram, scan, stable scatter ----------------------------------------------------
-__global__ __launch_bounds__(64) void mtu_count_kernel(MtuParams p) {
+__global__ __launch_bounds__(64) void mtu_count_kernel(MtuLaunch L) {
     __shared__ uint32_t hist[kMtuMaxShards + 1];
+    const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.tile0; });
+    const MtuParams p = mtu_view(L, bi);
     const int lane = threadIdx.x;
-    const uint32_t nk = p.nds + 1, t = blockIdx.x;
+    const uint32_t nk = p.nds + 1, t = blockIdx.x - L.b[bi].tile0;
     for (uint32_t k = lane; k < nk; k += 64) hist[k] = 0;
     __syncthreads();
     const uint32_t n = mtu_lines(p), r0 = t * kMtuTile;
@@ -99,7 +172,8 @@ __global__ __launch_bounds__(64) void mtu_count_kernel(MtuParams p) {
 
 // One workgroup of 1024 threads: exclusive scan of the key-major table (position of (key, tile)
 // = lines of smaller keys + lines of the same key in earlier tiles), key starts, packing chunks.
-__global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuParams p) {
+__global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuLaunch L) {
+    const MtuParams p = mtu_view(L, blockIdx.x);
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t carry_s;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -164,11 +238,13 @@ __global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuParams p) {
     }
 }
 
-__global__ __launch_bounds__(64) void mtu_scatter_kernel(MtuParams p) {
+__global__ __launch_bounds__(64) void mtu_scatter_kernel(MtuLaunch L) {
     __shared__ uint32_t pos[kMtuMaxShards + 1];
     volatile uint32_t *vpos = pos;
+    const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.tile0; });
+    const MtuParams p = mtu_view(L, bi);
     const int lane = threadIdx.x;
-    const uint32_t nk = p.nds + 1, t = blockIdx.x;
+    const uint32_t nk = p.nds + 1, t = blockIdx.x - L.b[bi].tile0;
     for (uint32_t k = lane; k < nk; k += 64) pos[k] = p.tile_counts[(size_t)k * p.ntiles + t];
     __syncthreads();
     const uint32_t n = mtu_lines(p), r0 = t * kMtuTile;
@@ -292,10 +368,12 @@ __device__ void mtu_chunk_build(const MtuParams &p, const MtuChunk &ck, MtuChunk
 }
 
 // table[c][x] = (packets closed << 32) | (last packet start << 16, 0xFFFF = none) | fill after
-__global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuParams p) {
+__global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
     __shared__ MtuChunkSmem sm;
     MtuChunk ck;
-    const uint32_t c = blockIdx.x;
+    const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.chunk0; });
+    const MtuParams p = mtu_view(L, bi);
+    const uint32_t c = blockIdx.x - L.b[bi].chunk0;
     if (!mtu_chunk_of(p, c, ck)) return;
     mtu_chunk_build(p, ck, sm, true);
     const uint32_t total = sm.P[ck.cnt - 1];
@@ -315,7 +393,8 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuParams p) {
 }
 
 // One workgroup: the chunks of every shard composed in order, descriptor slots scanned.
-__global__ __launch_bounds__(1024) void mtu_chain_kernel(MtuParams p) {
+__global__ __launch_bounds__(1024) void mtu_chain_kernel(MtuLaunch L) {
+    const MtuParams p = mtu_view(L, blockIdx.x);
     __shared__ uint32_t wsum[16];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t per = (p.nds + 1023) / 1024;
@@ -338,7 +417,7 @@ __global__ __launch_bounds__(1024) void mtu_chain_kernel(MtuParams p) {
         }
         p.fill_out[s] = mtu_dropped(p, s) ? 0 : (uint16_t)x;
         loc += closed + (c1 > c0 ? 1u : 0u);
-        p.chunk_entry[p.max_chunks + s] = closed;   // scratch: closed packets of s (after the chunk rows)
+        p.closed[s] = closed;
     }
     const uint32_t incl = wave_incl_add32(loc);
     if (lane == 63) wsum[wave] = incl;
@@ -348,7 +427,7 @@ __global__ __launch_bounds__(1024) void mtu_chain_kernel(MtuParams p) {
     for (uint32_t s = tid * per; s < (tid + 1) * per && s < p.nds; ++s) {
         const uint32_t c0 = p.chunk_first[s], c1 = min(p.chunk_first[s + 1], p.max_chunks);
         for (uint32_t c = c0; c < c1; ++c) p.chunk_pk[c] += run;
-        run += p.chunk_entry[p.max_chunks + s] + (c1 > c0 ? 1u : 0u);
+        run += p.closed[s] + (c1 > c0 ? 1u : 0u);
     }
     if (tid == 1023) p.counts[0] = run;
 }
@@ -367,11 +446,13 @@ __device__ __forceinline__ void mtu_put(const MtuParams &p, uint32_t k, uint32_t
     }
 }
 
-__global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuParams p) {
+__global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuLaunch L) {
     __shared__ MtuChunkSmem sm;
     __shared__ uint32_t nwalk, jfirst;
     MtuChunk ck;
-    const uint32_t c = blockIdx.x;
+    const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.chunk0; });
+    const MtuParams p = mtu_view(L, bi);
+    const uint32_t c = blockIdx.x - L.b[bi].chunk0;
     if (!mtu_chunk_of(p, c, ck)) return;
     mtu_chunk_build(p, ck, sm, false);
     const int tid = threadIdx.x;

@@ -303,76 +303,94 @@ int sr_pack_many_by_owner(sr_ctx *c, const sr_batch *batches, size_t count, uint
     return pack_launch(c, in, (uint32_t)count, n_owners, d_out_bytes, out_cap, d_out_recs, d_owner_counts);
 }
 
-// Scratch of the packing kernels for max_records records (grown, never shrunk; not in capture).
-static int mtu_reserve(sr_ctx *c, size_t max_records) {
+// Scratch of the packing kernels for one launch (grown, never shrunk; not in stream capture).
+static int mtu_reserve(sr_ctx *c, uint32_t tiles, uint32_t chunks, uint32_t nb) {
     const uint32_t nds = c->ds.nds;
-    const uint32_t ntiles = (uint32_t)((max_records + kMtuTile - 1) / kMtuTile) + 1;
-    const uint32_t chunks = (uint32_t)((max_records + kMtuChunk - 1) / kMtuChunk) + nds + 1;
-    if (ntiles > c->mtu_ntiles) {
+    if (tiles > c->mtu_ntiles) {
         free_ptr(c->d_mtu_tiles);
         c->d_mtu_tiles = nullptr;
         c->mtu_ntiles = 0;
-        if (hipMalloc(&c->d_mtu_tiles, (size_t)(nds + 1) * ntiles * sizeof(uint32_t)) != hipSuccess) return -ENOMEM;
-        c->mtu_ntiles = ntiles;
+        if (hipMalloc(&c->d_mtu_tiles, (size_t)(nds + 1) * tiles * sizeof(uint32_t)) != hipSuccess) return -ENOMEM;
+        c->mtu_ntiles = tiles;
     }
-    if (!c->d_mtu_keys && hipMalloc(&c->d_mtu_keys, (2 * (size_t)nds + 4) * sizeof(uint32_t)) != hipSuccess)
-        return -ENOMEM;
+    if (!c->d_mtu_keys) {   // keys and closed counts for the most batches a launch can hold
+        const size_t words = (size_t)kMtuMaxBatches * (2 * (size_t)nds + 4) + (size_t)kMtuMaxBatches * nds;
+        if (hipMalloc(&c->d_mtu_keys, words * sizeof(uint32_t)) != hipSuccess) return -ENOMEM;
+    }
+    (void)nb;
     if (chunks > c->mtu_chunks) {
         free_ptr(c->d_mtu_chunks);
         free_ptr(c->d_mtu_table);
         c->d_mtu_chunks = nullptr;
         c->d_mtu_table = nullptr;
         c->mtu_chunks = 0;
-        // shard, entry (+ nds scratch), open, first descriptor per chunk
-        if (hipMalloc(&c->d_mtu_chunks, (4 * (size_t)chunks + nds) * sizeof(uint32_t)) != hipSuccess) return -ENOMEM;
+        // shard, entry, open, first descriptor per chunk
+        if (hipMalloc(&c->d_mtu_chunks, 4 * (size_t)chunks * sizeof(uint32_t)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&c->d_mtu_table, (size_t)chunks * kMtuX * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
         c->mtu_chunks = chunks;
     }
     return 0;
 }
 
+int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) {
+    if (!c || !batches || count == 0 || count > (size_t)kMtuMaxBatches) return -EINVAL;
+    const uint32_t nds = c->ds.nds;
+    if (nds > SR_MAX_PACK_DOWNSTREAMS) return -EINVAL;
+    MtuLaunch L;
+    memset(&L, 0, sizeof(L));
+    uint32_t tiles = 0, chunks = 0;
+    for (size_t j = 0; j < count; ++j) {
+        const sr_pack_batch &b = batches[j];
+        if (!b.d_n_records || !b.d_counts || (nds && !b.d_fill_out) || b.max_records > 0xFFFFFFF0ull) return -EINVAL;
+        if (b.max_records && (!b.d_recs || !b.d_sorted)) return -EINVAL;
+        if (b.max_packets && !b.d_packets) return -EINVAL;
+        MtuBatchArg &a = L.b[j];
+        a.recs = b.d_recs;
+        a.n_records = b.d_n_records;
+        a.fill_in = b.d_fill_in;
+        a.probed_dead = b.d_probed_dead;
+        a.sorted = b.d_sorted;
+        a.packets = b.d_packets;
+        a.counts = b.d_counts;
+        a.fill_out = b.d_fill_out;
+        a.max_records = (uint32_t)b.max_records;
+        a.max_packets = (uint32_t)(b.max_packets > 0xFFFFFFFFull ? 0xFFFFFFFFull : b.max_packets);
+        a.tile0 = tiles;
+        a.chunk0 = chunks;
+        const uint64_t nt = (b.max_records + kMtuTile - 1) / kMtuTile;
+        tiles += (uint32_t)(nt ? nt : 1);
+        chunks += (uint32_t)((b.max_records + kMtuChunk - 1) / kMtuChunk) + nds + 1;
+    }
+    (void)hipSetDevice(c->device);
+    int rc = mtu_reserve(c, tiles, chunks, (uint32_t)count);
+    if (rc) return rc;
+    L.nds = nds;
+    L.nb = (uint32_t)count;
+    L.tiles = tiles;
+    L.chunks = chunks;
+    L.tile_counts = c->d_mtu_tiles;
+    L.keys = c->d_mtu_keys;
+    L.closed = c->d_mtu_keys + (size_t)kMtuMaxBatches * (2 * (size_t)nds + 4);
+    L.chunk_shard = c->d_mtu_chunks;
+    L.chunk_entry = c->d_mtu_chunks + (size_t)chunks;
+    L.chunk_open = c->d_mtu_chunks + 2 * (size_t)chunks;
+    L.chunk_pk = c->d_mtu_chunks + 3 * (size_t)chunks;
+    L.table = c->d_mtu_table;
+    hipLaunchKernelGGL(mtu_count_kernel, dim3(tiles), dim3(64), 0, c->stream, L);
+    hipLaunchKernelGGL(mtu_scan_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
+    hipLaunchKernelGGL(mtu_scatter_kernel, dim3(tiles), dim3(64), 0, c->stream, L);
+    hipLaunchKernelGGL(mtu_table_kernel, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
+    hipLaunchKernelGGL(mtu_chain_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
+    hipLaunchKernelGGL(mtu_emit_kernel, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
+    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
 int sr_pack_packets(sr_ctx *c, const sr_record *d_recs, const uint64_t *d_n_records, size_t max_records,
                     const uint16_t *d_fill_in, const uint64_t *d_probed_dead, sr_record *d_sorted,
                     sr_packet *d_packets, size_t max_packets, uint64_t *d_counts, uint16_t *d_fill_out) {
-    if (!c || !d_n_records || !d_counts || (c->ds.nds && !d_fill_out)) return -EINVAL;
-    if (c->ds.nds > SR_MAX_PACK_DOWNSTREAMS || max_records > 0xFFFFFFF0ull) return -EINVAL;
-    if (max_records && (!d_recs || !d_sorted)) return -EINVAL;
-    if (max_packets && !d_packets) return -EINVAL;
-    (void)hipSetDevice(c->device);
-    int rc = mtu_reserve(c, max_records);
-    if (rc) return rc;
-    const uint32_t nds = c->ds.nds;
-    MtuParams p;
-    memset(&p, 0, sizeof(p));
-    p.recs = d_recs;
-    p.n_records = d_n_records;
-    p.max_records = (uint32_t)max_records;
-    p.nds = nds;
-    p.ntiles = (uint32_t)((max_records + kMtuTile - 1) / kMtuTile);
-    if (p.ntiles == 0) p.ntiles = 1;
-    p.max_chunks = (uint32_t)((max_records + kMtuChunk - 1) / kMtuChunk) + nds;
-    p.fill_in = d_fill_in;
-    p.probed_dead = d_probed_dead;
-    p.tile_counts = c->d_mtu_tiles;
-    p.key_start = c->d_mtu_keys;
-    p.chunk_first = c->d_mtu_keys + nds + 2;
-    p.chunk_shard = c->d_mtu_chunks;
-    p.chunk_entry = c->d_mtu_chunks + p.max_chunks;           // + nds scratch words after the chunk rows
-    p.chunk_open = p.chunk_entry + p.max_chunks + nds;
-    p.chunk_pk = p.chunk_open + p.max_chunks;
-    p.table = c->d_mtu_table;
-    p.sorted = d_sorted;
-    p.packets = d_packets;
-    p.max_packets = max_packets;
-    p.counts = d_counts;
-    p.fill_out = d_fill_out;
-    hipLaunchKernelGGL(mtu_count_kernel, dim3(p.ntiles), dim3(64), 0, c->stream, p);
-    hipLaunchKernelGGL(mtu_scan_kernel, dim3(1), dim3(1024), 0, c->stream, p);
-    hipLaunchKernelGGL(mtu_scatter_kernel, dim3(p.ntiles), dim3(64), 0, c->stream, p);
-    if (p.max_chunks) hipLaunchKernelGGL(mtu_table_kernel, dim3(p.max_chunks), dim3(kMtuBlock), 0, c->stream, p);
-    hipLaunchKernelGGL(mtu_chain_kernel, dim3(1), dim3(1024), 0, c->stream, p);
-    if (p.max_chunks) hipLaunchKernelGGL(mtu_emit_kernel, dim3(p.max_chunks), dim3(kMtuBlock), 0, c->stream, p);
-    return hipGetLastError() == hipSuccess ? 0 : -EIO;
+    const sr_pack_batch b{d_recs, d_n_records, max_records, d_fill_in, d_probed_dead,
+                          d_sorted, d_packets, max_packets, d_counts, d_fill_out};
+    return sr_pack_packets_many(c, &b, 1);
 }
 
 static int grow(void **ptr, size_t *cap, size_t need, size_t elem) {

@@ -185,3 +185,49 @@ def test_route_pack_edges(pkg, oracle):
                     assert len(srt) == 0 and len(pk) == 0 and fo.tolist() == fill
                     continue
                 _check_pack(pkg, oracle, data, n, None, fill, r)
+
+
+def test_pack_packets_many_independent_batches(pkg, oracle, torch_stream):
+    """sr_pack_packets_many: the batches of several data threads packed in one set of launches,
+    each from its own pending bytes, equal the oracle batch by batch."""
+    import torch
+
+    n, nb, size = 16, 7, 1 << 19
+    alive = [int(k % 6 != 2) for k in range(n)]
+    rng = np.random.default_rng(17)
+    streams = [pkg.gen_stream(size - 1000 * b, [[64], [256], [1024], [64, 256, 1024], [6, 13]][b % 5],
+                              seed=1300 + b, p_invalid=0.05) for b in range(nb)]
+    cap = max(s.n_lines for s in streams)
+    d_in = torch.zeros((nb, size), dtype=torch.uint8, device="cuda")
+    for b, s in enumerate(streams):
+        d_in[b, : s.data.size].copy_(torch.from_numpy(s.data))
+    d_rec = torch.zeros((nb, cap), dtype=torch.int64, device="cuda")
+    d_cnt = torch.zeros(nb, dtype=torch.int64, device="cuda")
+    d_pd = torch.zeros((nb, 1), dtype=torch.int64, device="cuda")
+    mp = pkg.max_packets(size, n)
+    d_srt = torch.zeros((nb, cap), dtype=torch.int64, device="cuda")
+    d_pk = torch.zeros((nb, mp * 2), dtype=torch.int64, device="cuda")
+    d_counts = torch.zeros((nb, 3), dtype=torch.int64, device="cuda")
+    fills = rng.integers(0, 1451, (nb, n)).astype(np.uint16)
+    d_fin = torch.from_numpy(fills.view(np.int16)).cuda()
+    d_fout = torch.zeros((nb, n), dtype=torch.int16, device="cuda")
+    with pkg.Router(n, size) as r:
+        r.set_alive(alive)
+        r.set_stream(torch_stream.cuda_stream)
+        r.route_device_many([(d_in[b].data_ptr(), int(s.data.size), d_rec[b].data_ptr(), cap, None,
+                              d_cnt[b].data_ptr(), d_pd[b].data_ptr()) for b, s in enumerate(streams)])
+        r.pack_packets_many([(d_rec[b].data_ptr(), d_cnt[b].data_ptr(), cap, d_fin[b].data_ptr(), d_pd[b].data_ptr(),
+                              d_srt[b].data_ptr(), d_pk[b].data_ptr(), mp, d_counts[b].data_ptr(),
+                              d_fout[b].data_ptr()) for b in range(nb)])
+        torch.cuda.synchronize()
+    for b, s in enumerate(streams):
+        recs, _, cnt = oracle.route(s.data, n, alive)
+        probed = oracle.probed_dead(s.data, n, alive)
+        srt_o, pk_o, fill_o, nv = oracle.pack_packets(recs, n, fills[b], probed)
+        np_, nv_g, nl = d_counts[b].cpu().tolist()
+        assert (np_, nv_g, nl) == (len(pk_o), nv, cnt), b
+        srt = np.frombuffer(d_srt[b].cpu().numpy().tobytes(), dtype=pkg.RECORD_DTYPE)[:cnt]
+        pk = np.frombuffer(d_pk[b].cpu().numpy().tobytes(), dtype=pkg.PACKET_DTYPE)[:np_]
+        assert np.array_equal(srt, srt_o), b
+        assert np.array_equal(pk.view(np.uint8), pk_o.view(np.uint8)), b
+        assert d_fout[b].cpu().numpy().view(np.uint16).tolist() == fill_o.tolist(), b
