@@ -29,7 +29,8 @@
 //               possible incoming fill x in 0..1450: packets closed, last start, fill out;
 //   mtu_chain   one workgroup: per shard, the chunks' tables composed in order from fill_in
 //               (one table read per chunk), packet counts scanned into descriptor slots;
-//   mtu_emit    per chunk: walks its packet chain from its incoming fill and writes descriptors.
+//   mtu_emit    per chunk: walks its packet chain from its incoming fill (one wave, next() in
+//               registers by 64-line windows) and writes descriptors.
 // Integer/byte work, latency-light: no MFMA.
 #pragma once
 
@@ -49,6 +50,12 @@ constexpr uint32_t kMtuNone = 0xFFFFFFFFu;
 constexpr uint16_t kMtuEnd = 0xFFFFu;
 
 constexpr int kMtuMaxBatches = 32;
+
+// Developer ablation mask for timing the chunk kernels' phases (tools/ab_mtu.sh; results are wrong
+// when set, never shipped): 1 doubling, 2 table fills, 4 emit walk, 8 next(), 16 prefix sums.
+#ifndef SR_MTU_SKIP
+#define SR_MTU_SKIP 0
+#endif
 
 // One batch of a packing launch (user buffers). Batches are independent: each has its own pending
 // bytes in and out (the downstream arrays of different data threads).
@@ -156,16 +163,36 @@ __device__ __forceinline__ bool mtu_dropped(const MtuParams &p, uint32_t s) {
 }
 
 // ---- sort: histogram, scan, stable scatter ----------------------------------------------------
+// The tile's records, loaded up front (kMtuTile / 64 independent loads in flight per lane rather
+// than one round trip per 64 records); key nds + 1 for positions past the batch.
+constexpr int kMtuPerLane = kMtuTile / 64;
+__device__ __forceinline__ void mtu_load_tile(const MtuParams &p, uint32_t r0, uint32_t n, int lane,
+                                              sr_record (&r)[kMtuPerLane]) {
+#pragma unroll
+    for (int k = 0; k < kMtuPerLane; ++k) {
+        const uint32_t i = r0 + (uint32_t)(64 * k + lane);
+        r[k] = i < n ? p.recs[i] : sr_record{0, 0, 0};
+    }
+}
+
+// LDS of the sort kernels: (nds + 1) counters, sized at launch (dynamic), so that small downstream
+// counts do not cap the resident waves
 __global__ __launch_bounds__(64) void mtu_count_kernel(MtuLaunch L) {
-    __shared__ uint32_t hist[kMtuMaxShards + 1];
+    extern __shared__ uint32_t hist[];
     const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.tile0; });
     const MtuParams p = mtu_view(L, bi);
     const int lane = threadIdx.x;
     const uint32_t nk = p.nds + 1, t = blockIdx.x - L.b[bi].tile0;
+    const uint32_t n = mtu_lines(p), r0 = t * kMtuTile;
+    sr_record r[kMtuPerLane];
+    if (r0 < n) mtu_load_tile(p, r0, n, lane, r);
     for (uint32_t k = lane; k < nk; k += 64) hist[k] = 0;
     __syncthreads();
-    const uint32_t n = mtu_lines(p), r0 = t * kMtuTile;
-    for (uint32_t i = r0 + lane; i < r0 + kMtuTile && i < n; i += 64) atomicAdd(&hist[mtu_key(p.recs[i], p.nds)], 1u);
+    if (r0 < n) {
+#pragma unroll
+        for (int k = 0; k < kMtuPerLane; ++k)
+            if (r0 + (uint32_t)(64 * k + lane) < n) atomicAdd(&hist[mtu_key(r[k], p.nds)], 1u);
+    }
     __syncthreads();
     for (uint32_t k = lane; k < nk; k += 64) p.tile_counts[(size_t)k * p.ntiles + t] = hist[k];
 }
@@ -239,25 +266,25 @@ __global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuLaunch L) {
 }
 
 __global__ __launch_bounds__(64) void mtu_scatter_kernel(MtuLaunch L) {
-    __shared__ uint32_t pos[kMtuMaxShards + 1];
+    extern __shared__ uint32_t pos[];
     volatile uint32_t *vpos = pos;
     const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.tile0; });
     const MtuParams p = mtu_view(L, bi);
     const int lane = threadIdx.x;
     const uint32_t nk = p.nds + 1, t = blockIdx.x - L.b[bi].tile0;
+    const uint32_t n = mtu_lines(p), r0 = t * kMtuTile;
+    if (r0 >= n) return;
+    sr_record rr[kMtuPerLane];
+    mtu_load_tile(p, r0, n, lane, rr);
     for (uint32_t k = lane; k < nk; k += 64) pos[k] = p.tile_counts[(size_t)k * p.ntiles + t];
     __syncthreads();
-    const uint32_t n = mtu_lines(p), r0 = t * kMtuTile;
     const uint64_t lt = (1ull << lane) - 1ull;
-    for (uint32_t c0 = r0; c0 < r0 + kMtuTile && c0 < n; c0 += 64) {
-        const uint32_t i = c0 + lane;
+#pragma unroll
+    for (int ck = 0; ck < kMtuPerLane; ++ck) {
+        const uint32_t i = r0 + (uint32_t)(64 * ck + lane);
         bool pend = i < n;
-        sr_record r{0, 0, 0};
-        uint32_t key = 0;
-        if (pend) {
-            r = p.recs[i];
-            key = mtu_key(r, p.nds);
-        }
+        const sr_record r = rr[ck];
+        const uint32_t key = pend ? mtu_key(r, p.nds) : 0u;
         // stable in-wave ranks: one round per distinct key of the 64 records
         for (uint64_t pm = __ballot(pend); pm; pm = __ballot(pend)) {
             const int leader = __builtin_ctzll(pm);
@@ -276,13 +303,16 @@ __global__ __launch_bounds__(64) void mtu_scatter_kernel(MtuLaunch L) {
 }
 
 // ---- packing: per-chunk next-fit tables -------------------------------------------------------
-struct MtuChunkSmem {
+// LDS of the two chunk kernels, kept apart so that each holds only what it reads (32 KiB: five
+// workgroups per CU instead of three; 20 KiB for emit). The prefix scan's wave sums borrow lst / nx.
+struct MtuTableSmem {
     uint32_t P[kMtuChunk];      // inclusive prefix of the chunk's line lengths
-    uint16_t nx[kMtuChunk];     // chunk-local start of the packet after one starting here, kMtuEnd
     uint16_t lst[kMtuChunk];    // last packet start reached from here
     uint16_t dep[kMtuChunk];    // packets closed on the way
-    uint32_t wsum[kMtuBlock / 64];
-    uint16_t walk[kMtuChunk + 1];
+};
+struct MtuEmitSmem {
+    uint32_t P[kMtuChunk];
+    uint8_t nx[kMtuChunk];      // next(i) - i (1 .. kMtuWindow - 1), 0 = none in the chunk
 };
 
 struct MtuChunk {
@@ -310,40 +340,95 @@ __device__ __forceinline__ uint32_t mtu_first_over(const uint32_t *P, uint32_t l
     return lo;
 }
 
-// LDS prefix sums of the chunk's lengths and next(i) for every line
-__device__ void mtu_chunk_build(const MtuParams &p, const MtuChunk &ck, MtuChunkSmem &sm, bool doubling) {
+// LDS prefix sums of the chunk's lengths: coalesced record loads staged through P, then each
+// thread scans its kMtuPer consecutive lines.
+__device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuChunk &ck, uint32_t *P,
+                                                 uint32_t *wsum) {
+    if (SR_MTU_SKIP & 16) {
+        for (uint32_t i = threadIdx.x; i < (uint32_t)kMtuChunk; i += kMtuBlock) P[i] = 64u * (i + 1);
+        __syncthreads();
+        return;
+    }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    uint32_t len[kMtuPer];
+#pragma unroll
+    for (int k = 0; k < kMtuPer; ++k) {
+        const uint32_t i = (uint32_t)tid + (uint32_t)k * kMtuBlock;
+        len[k] = i < ck.cnt ? p.sorted[ck.pos0 + i].length : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kMtuPer; ++k) P[tid + k * kMtuBlock] = len[k];
+    __syncthreads();
     uint32_t v[kMtuPer], s = 0;
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) {
-        const uint32_t i = (uint32_t)tid * kMtuPer + k;
-        v[k] = i < ck.cnt ? p.sorted[ck.pos0 + i].length : 0u;
+        v[k] = P[tid * kMtuPer + k];
         s += v[k];
     }
     const uint32_t incl = wave_incl_add32(s);
-    if (lane == 63) sm.wsum[wave] = incl;
+    if (lane == 63) wsum[wave] = incl;
     __syncthreads();
     uint32_t run = incl - s;
-    for (int w = 0; w < wave; ++w) run += sm.wsum[w];
+    for (int w = 0; w < wave; ++w) run += wsum[w];
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) {
         run += v[k];
-        sm.P[tid * kMtuPer + k] = run;
+        P[tid * kMtuPer + k] = run;
     }
     __syncthreads();
-    for (uint32_t i = tid; i < ck.cnt; i += kMtuBlock) {
-        const uint32_t pm = i ? sm.P[i - 1] : 0u;
-        const uint32_t hi = min(ck.cnt, i + (uint32_t)kMtuWindow);
-        uint16_t nxt = kMtuEnd;
-        if (sm.P[hi - 1] - pm > (uint32_t)kMtuCap) nxt = (uint16_t)mtu_first_over(sm.P, i + 1, hi - 1, pm + kMtuCap);
-        sm.nx[i] = nxt;
+}
+
+// next(i) for the thread's consecutive lines i0 .. i0 + kMtuPer - 1: next is monotone in i, so
+// one binary search for the first line, then a forward scan. f(i, next) stores the result.
+template <typename F>
+__device__ __forceinline__ void mtu_chunk_next(const uint32_t *P, uint32_t cnt, F f) {
+    const uint32_t i0 = (uint32_t)threadIdx.x * kMtuPer;
+    if (i0 >= cnt) return;
+    if (SR_MTU_SKIP & 8) {
+        for (uint32_t i = i0; i < i0 + kMtuPer && i < cnt; ++i) f(i, i + 22 < cnt ? (uint16_t)(i + 22) : kMtuEnd);
+        return;
+    }
+    const uint32_t total = P[cnt - 1];
+    uint32_t j = 0;
+    bool end = false;
+    for (uint32_t i = i0; i < i0 + kMtuPer && i < cnt; ++i) {
+        const uint32_t lim = (i ? P[i - 1] : 0u) + (uint32_t)kMtuCap;
+        if (!end && total <= lim) end = true;   // every later line fits too
+        if (end) {
+            f(i, kMtuEnd);
+            continue;
+        }
+        if (i == i0) {
+            j = mtu_first_over(P, i + 1, min(cnt, i + (uint32_t)kMtuWindow) - 1, lim);
+        } else {
+            if (j <= i) j = i + 1;
+            while (P[j] <= lim) ++j;   // bounded: P[cnt - 1] > lim
+        }
+        f(i, (uint16_t)j);
+    }
+}
+
+// table[c][x] = (packets closed << 32) | (last packet start << 16, 0xFFFF = none) | fill after
+__global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
+    __shared__ MtuTableSmem sm;
+    MtuChunk ck;
+    const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.chunk0; });
+    const MtuParams p = mtu_view(L, bi);
+    const uint32_t c = blockIdx.x - L.b[bi].chunk0;
+    if (!mtu_chunk_of(p, c, ck)) return;
+    const int tid = threadIdx.x;
+    mtu_chunk_prefix(p, ck, sm.P, reinterpret_cast<uint32_t *>(sm.lst));
+    mtu_chunk_next(sm.P, ck.cnt, [&](uint32_t i, uint16_t nxt) {
         sm.lst[i] = nxt == kMtuEnd ? (uint16_t)i : nxt;
         sm.dep[i] = nxt == kMtuEnd ? 0 : 1;
-    }
+    });
     __syncthreads();
-    if (!doubling) return;
-    // pointer doubling: lst -> the last packet start of the chain, dep -> packets closed on it
-    for (uint32_t span = 1; span < ck.cnt; span <<= 1) {
+    const uint32_t total = sm.P[ck.cnt - 1];
+    // pointer doubling: lst -> the last packet start of the chain, dep -> packets closed on it.
+    // A chain closes at most 2 * total / (cap + 1) + 1 packets (two consecutive closed packets
+    // exceed the cap together), so that many jumps suffice.
+    const uint32_t kb = min(ck.cnt, 2u * total / (uint32_t)(kMtuCap + 1) + 2u);
+    for (uint32_t span = 1; !(SR_MTU_SKIP & 1) && span < kb; span <<= 1) {
         uint16_t nl[kMtuPer], nd[kMtuPer];
 #pragma unroll
         for (int k = 0; k < kMtuPer; ++k) {
@@ -365,26 +450,25 @@ __device__ void mtu_chunk_build(const MtuParams &p, const MtuChunk &ck, MtuChunk
         }
         __syncthreads();
     }
-}
-
-// table[c][x] = (packets closed << 32) | (last packet start << 16, 0xFFFF = none) | fill after
-__global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
-    __shared__ MtuChunkSmem sm;
-    MtuChunk ck;
-    const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.chunk0; });
-    const MtuParams p = mtu_view(L, bi);
-    const uint32_t c = blockIdx.x - L.b[bi].chunk0;
-    if (!mtu_chunk_of(p, c, ck)) return;
-    mtu_chunk_build(p, ck, sm, true);
-    const uint32_t total = sm.P[ck.cnt - 1];
+    // incoming fills x0 .. x0 + per - 1 per thread: the first line over the cap moves down with x
+    constexpr uint32_t per = (kMtuX + kMtuBlock - 1) / kMtuBlock;
     const uint32_t hi = min(ck.cnt, (uint32_t)kMtuWindow);
     uint64_t *row = p.table + (size_t)c * kMtuX;
-    for (uint32_t x = threadIdx.x; x < (uint32_t)kMtuX; x += kMtuBlock) {
+    const uint32_t x0 = (uint32_t)tid * per;
+    uint32_t j = 0;
+    bool first = true;
+    for (uint32_t x = x0; !(SR_MTU_SKIP & 2) && x < x0 + per && x < (uint32_t)kMtuX; ++x) {
         uint64_t e;
         if (x + total <= (uint32_t)kMtuCap) {
             e = (0xFFFFull << 16) | (x + total);
         } else {
-            const uint32_t j = mtu_first_over(sm.P, 0, hi - 1, (uint32_t)kMtuCap - x);
+            const uint32_t lim = (uint32_t)kMtuCap - x;
+            if (first) {
+                j = mtu_first_over(sm.P, 0, hi - 1, lim);
+                first = false;
+            } else {
+                while (j > 0 && sm.P[j - 1] > lim) --j;
+            }
             const uint32_t l = sm.lst[j];
             e = ((uint64_t)(1u + sm.dep[j]) << 32) | ((uint64_t)l << 16) | (total - (l ? sm.P[l - 1] : 0u));
         }
@@ -446,52 +530,63 @@ __device__ __forceinline__ void mtu_put(const MtuParams &p, uint32_t k, uint32_t
     }
 }
 
+// The chunk's packet chain (the first line that does not fit the incoming packet, then next())
+// is walked by one wave over 64-line windows of next() held in registers: each step is a lane
+// read, not an LDS round trip; the chain members of a window then write their descriptors.
 __global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuLaunch L) {
-    __shared__ MtuChunkSmem sm;
-    __shared__ uint32_t nwalk, jfirst;
+    __shared__ MtuEmitSmem sm;
     MtuChunk ck;
     const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.chunk0; });
     const MtuParams p = mtu_view(L, bi);
     const uint32_t c = blockIdx.x - L.b[bi].chunk0;
     if (!mtu_chunk_of(p, c, ck)) return;
-    mtu_chunk_build(p, ck, sm, false);
-    const int tid = threadIdx.x;
+    mtu_chunk_prefix(p, ck, sm.P, reinterpret_cast<uint32_t *>(sm.nx));
+    mtu_chunk_next(sm.P, ck.cnt, [&](uint32_t i, uint16_t nxt) { sm.nx[i] = nxt == kMtuEnd ? 0 : (uint8_t)(nxt - i); });
+    __syncthreads();
+    if (threadIdx.x >= 64) return;
+    const uint32_t lane = threadIdx.x;
     const uint32_t x = p.chunk_entry[c], open = p.chunk_open[c], k0 = p.chunk_pk[c];
     const uint32_t total = sm.P[ck.cnt - 1];
     const uint32_t carry = open == kMtuNone ? x : 0u;        // pending bytes from before the batch
     const uint32_t start = open == kMtuNone ? p.key_start[ck.shard] : open;
-    if (tid == 0) {
-        // the chain of packet starts: the first line that does not fit the incoming packet, then next()
-        uint32_t nw = 0;
-        uint32_t j = kMtuEnd;
-        if (x + total > (uint32_t)kMtuCap) {
-            j = mtu_first_over(sm.P, 0, min(ck.cnt, (uint32_t)kMtuWindow) - 1, (uint32_t)kMtuCap - x);
-            for (uint32_t cur = j;; cur = sm.nx[cur]) {
-                sm.walk[nw++] = (uint16_t)cur;
-                if (sm.nx[cur] == kMtuEnd) break;
-            }
-        }
-        nwalk = nw;
-        jfirst = j;
-    }
-    __syncthreads();
-    const uint32_t nw = nwalk;
-    if (nw == 0) {   // no line of the chunk closes a packet: the incoming one stays open
-        if (ck.last && tid == 0)
+    if (x + total <= (uint32_t)kMtuCap) {   // no line of the chunk closes a packet: the incoming one stays open
+        if (ck.last && lane == 0)
             mtu_put(p, k0, start, ck.pos0 + ck.cnt - start, ck.shard, x - carry + total, carry, 1u);
         return;
     }
-    if (tid == 0) {   // the incoming packet closes before line jfirst
-        const uint32_t j = jfirst;
+    const uint32_t j = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)mtu_first_over(sm.P, 0, min(ck.cnt, (uint32_t)kMtuWindow) - 1, (uint32_t)kMtuCap - x));
+    if (lane == 0)   // the incoming packet closes before line j
         mtu_put(p, k0, start, ck.pos0 + j - start, ck.shard, x - carry + (j ? sm.P[j - 1] : 0u), carry, 0u);
-    }
-    for (uint32_t w = tid; w < nw; w += kMtuBlock) {
-        const uint32_t a = sm.walk[w];
-        const bool is_open = w + 1 == nw;
-        if (is_open && !ck.last) continue;   // continues into the next chunk
-        const uint32_t b = is_open ? ck.cnt : sm.walk[w + 1];
-        mtu_put(p, k0 + 1 + w, ck.pos0 + a, b - a, ck.shard, sm.P[b - 1] - (a ? sm.P[a - 1] : 0u), 0u,
-                is_open ? 1u : 0u);
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t w = 0;
+    for (uint32_t base = j; !(SR_MTU_SKIP & 4);) {
+        const uint32_t a = base + lane;
+        const uint32_t d = a < ck.cnt ? (uint32_t)sm.nx[a] : 0u;
+        uint64_t mask = 0;
+        uint32_t off = 0;
+        bool done = false;
+        for (;;) {
+            mask |= 1ull << off;
+            const uint32_t dd = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)off);
+            if (dd == 0) {
+                done = true;
+                break;
+            }
+            off += dd;
+            if (off >= 64) break;
+        }
+        if ((mask >> lane) & 1ull) {
+            const bool is_open = d == 0;   // the last packet start: the packet stays pending
+            if (!is_open || ck.last) {     // else it continues into the next chunk
+                const uint32_t b = is_open ? ck.cnt : a + d;
+                mtu_put(p, k0 + 1 + w + (uint32_t)__popcll(mask & lt), ck.pos0 + a, b - a, ck.shard,
+                        sm.P[b - 1] - (a ? sm.P[a - 1] : 0u), 0u, is_open ? 1u : 0u);
+            }
+        }
+        w += (uint32_t)__popcll(mask);
+        if (done) break;
+        base += off;
     }
 }
 

@@ -376,9 +376,10 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     L.chunk_open = c->d_mtu_chunks + 2 * (size_t)chunks;
     L.chunk_pk = c->d_mtu_chunks + 3 * (size_t)chunks;
     L.table = c->d_mtu_table;
-    hipLaunchKernelGGL(mtu_count_kernel, dim3(tiles), dim3(64), 0, c->stream, L);
+    const size_t sort_lds = (size_t)(nds + 1) * sizeof(uint32_t);
+    hipLaunchKernelGGL(mtu_count_kernel, dim3(tiles), dim3(64), sort_lds, c->stream, L);
     hipLaunchKernelGGL(mtu_scan_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
-    hipLaunchKernelGGL(mtu_scatter_kernel, dim3(tiles), dim3(64), 0, c->stream, L);
+    hipLaunchKernelGGL(mtu_scatter_kernel, dim3(tiles), dim3(64), sort_lds, c->stream, L);
     hipLaunchKernelGGL(mtu_table_kernel, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
     hipLaunchKernelGGL(mtu_chain_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
     hipLaunchKernelGGL(mtu_emit_kernel, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
