@@ -84,6 +84,7 @@ struct MtuLaunch {
     uint32_t *chunk_pk;                // [chunks] first descriptor the chunk writes
     uint32_t *closed;                  // [nb][nds] packets closed per shard
     uint64_t *table;                   // [chunks][kMtuX]
+    uint8_t *nx;                       // [chunks][kMtuChunk] next(i) - i per line (mtu_table -> mtu_emit)
     MtuBatchArg b[kMtuMaxBatches];
 };
 static_assert(sizeof(MtuLaunch) < 3584, "kernel argument size");
@@ -103,6 +104,7 @@ struct MtuParams {
     uint32_t *chunk_first;    // [nds + 1]: first chunk of each shard, [nds] = chunks
     uint32_t *chunk_shard;
     uint64_t *table;
+    uint8_t *nx;
     uint32_t *chunk_entry;
     uint32_t *chunk_open;     // kMtuNone: the incoming packet began before the batch
     uint32_t *chunk_pk;
@@ -130,6 +132,7 @@ __device__ __forceinline__ MtuParams mtu_view(const MtuLaunch &L, uint32_t bi) {
     p.chunk_first = p.key_start + L.nds + 2;
     p.chunk_shard = L.chunk_shard + a.chunk0;
     p.table = L.table + (size_t)a.chunk0 * kMtuX;
+    p.nx = L.nx + (size_t)a.chunk0 * kMtuChunk;
     p.chunk_entry = L.chunk_entry + a.chunk0;
     p.chunk_open = L.chunk_open + a.chunk0;
     p.chunk_pk = L.chunk_pk + a.chunk0;
@@ -304,15 +307,14 @@ __global__ __launch_bounds__(64) void mtu_scatter_kernel(MtuLaunch L) {
 
 // ---- packing: per-chunk next-fit tables -------------------------------------------------------
 // LDS of the two chunk kernels, kept apart so that each holds only what it reads (32 KiB: five
-// workgroups per CU instead of three; 20 KiB for emit). The prefix scan's wave sums borrow lst / nx.
+// workgroups per CU instead of three; 20 KiB for emit). The prefix scan's wave sums borrow ld / nx.
 struct MtuTableSmem {
     uint32_t P[kMtuChunk];      // inclusive prefix of the chunk's line lengths
-    uint16_t lst[kMtuChunk];    // last packet start reached from here
-    uint16_t dep[kMtuChunk];    // packets closed on the way
+    uint32_t ld[kMtuChunk];     // last packet start reached from here << 16 | packets closed on the way
 };
 struct MtuEmitSmem {
     uint32_t P[kMtuChunk];
-    uint8_t nx[kMtuChunk];      // next(i) - i (1 .. kMtuWindow - 1), 0 = none in the chunk
+    alignas(16) uint8_t nx[kMtuChunk];   // next(i) - i (1 .. kMtuWindow - 1), 0 = none in the chunk
 };
 
 struct MtuChunk {
@@ -340,8 +342,9 @@ __device__ __forceinline__ uint32_t mtu_first_over(const uint32_t *P, uint32_t l
     return lo;
 }
 
-// LDS prefix sums of the chunk's lengths: coalesced record loads staged through P, then each
-// thread scans its kMtuPer consecutive lines.
+// LDS prefix sums of the chunk's lengths. Wave w owns lines [1024 w, 1024 w + 1024), lane-
+// interleaved (line 1024 w + 64 k + lane): coalesced record loads, conflict-free LDS stores, the
+// running sum carried across the wave's 16 rows by DPP scans; one barrier for the wave offsets.
 __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuChunk &ck, uint32_t *P,
                                                  uint32_t *wsum) {
     if (SR_MTU_SKIP & 16) {
@@ -350,61 +353,58 @@ __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuCh
         return;
     }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    uint32_t len[kMtuPer];
+    const uint32_t base = (uint32_t)wave * (kMtuChunk / (kMtuBlock / 64)) + (uint32_t)lane;
+    uint32_t v[kMtuPer];
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) {
-        const uint32_t i = (uint32_t)tid + (uint32_t)k * kMtuBlock;
-        len[k] = i < ck.cnt ? p.sorted[ck.pos0 + i].length : 0u;
+        const uint32_t i = base + 64u * k;
+        v[k] = i < ck.cnt ? p.sorted[ck.pos0 + i].length : 0u;
     }
+    uint32_t carry = 0;
 #pragma unroll
-    for (int k = 0; k < kMtuPer; ++k) P[tid + k * kMtuBlock] = len[k];
+    for (int k = 0; k < kMtuPer; ++k) {
+        v[k] = wave_incl_add32(v[k]) + carry;
+        carry = (uint32_t)__builtin_amdgcn_readlane((int)v[k], 63);
+    }
+    if (lane == 63) wsum[wave] = carry;
     __syncthreads();
-    uint32_t v[kMtuPer], s = 0;
+    uint32_t add = 0;
+    for (int w = 0; w < wave; ++w) add += wsum[w];
 #pragma unroll
-    for (int k = 0; k < kMtuPer; ++k) {
-        v[k] = P[tid * kMtuPer + k];
-        s += v[k];
-    }
-    const uint32_t incl = wave_incl_add32(s);
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t run = incl - s;
-    for (int w = 0; w < wave; ++w) run += wsum[w];
-#pragma unroll
-    for (int k = 0; k < kMtuPer; ++k) {
-        run += v[k];
-        P[tid * kMtuPer + k] = run;
-    }
+    for (int k = 0; k < kMtuPer; ++k) P[base + 64u * k] = v[k] + add;
     __syncthreads();
 }
 
-// next(i) for the thread's consecutive lines i0 .. i0 + kMtuPer - 1: next is monotone in i, so
-// one binary search for the first line, then a forward scan. f(i, next) stores the result.
+// next(i) = the first line that no longer fits a packet starting at line i (kMtuEnd: none in the
+// chunk), for lines tid + 256 k: a fixed 8-step search over the 256 lines after i (a packet holds
+// fewer than 242), the 16 searches of a thread independent, neighbouring lanes on neighbouring
+// words. f(i, next) stores the result.
 template <typename F>
 __device__ __forceinline__ void mtu_chunk_next(const uint32_t *P, uint32_t cnt, F f) {
-    const uint32_t i0 = (uint32_t)threadIdx.x * kMtuPer;
-    if (i0 >= cnt) return;
     if (SR_MTU_SKIP & 8) {
-        for (uint32_t i = i0; i < i0 + kMtuPer && i < cnt; ++i) f(i, i + 22 < cnt ? (uint16_t)(i + 22) : kMtuEnd);
+        for (uint32_t i = threadIdx.x; i < cnt; i += kMtuBlock) f(i, i + 22 < cnt ? (uint16_t)(i + 22) : kMtuEnd);
         return;
     }
     const uint32_t total = P[cnt - 1];
-    uint32_t j = 0;
-    bool end = false;
-    for (uint32_t i = i0; i < i0 + kMtuPer && i < cnt; ++i) {
-        const uint32_t lim = (i ? P[i - 1] : 0u) + (uint32_t)kMtuCap;
-        if (!end && total <= lim) end = true;   // every later line fits too
-        if (end) {
-            f(i, kMtuEnd);
-            continue;
+    uint32_t lo[kMtuPer], lim[kMtuPer];
+#pragma unroll
+    for (int k = 0; k < kMtuPer; ++k) {
+        const uint32_t i = threadIdx.x + (uint32_t)k * kMtuBlock;
+        lo[k] = i;   // P[i] <= lim: a line alone always fits
+        lim[k] = (i && i < cnt ? P[i - 1] : 0u) + (uint32_t)kMtuCap;
+    }
+#pragma unroll
+    for (uint32_t step = 128; step; step >>= 1) {
+#pragma unroll
+        for (int k = 0; k < kMtuPer; ++k) {
+            const uint32_t t = lo[k] + step;
+            if (t < cnt && P[t] <= lim[k]) lo[k] = t;
         }
-        if (i == i0) {
-            j = mtu_first_over(P, i + 1, min(cnt, i + (uint32_t)kMtuWindow) - 1, lim);
-        } else {
-            if (j <= i) j = i + 1;
-            while (P[j] <= lim) ++j;   // bounded: P[cnt - 1] > lim
-        }
-        f(i, (uint16_t)j);
+    }
+#pragma unroll
+    for (int k = 0; k < kMtuPer; ++k) {
+        const uint32_t i = threadIdx.x + (uint32_t)k * kMtuBlock;
+        if (i < cnt) f(i, total <= lim[k] ? kMtuEnd : (uint16_t)(lo[k] + 1));
     }
 }
 
@@ -417,35 +417,27 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
     const uint32_t c = blockIdx.x - L.b[bi].chunk0;
     if (!mtu_chunk_of(p, c, ck)) return;
     const int tid = threadIdx.x;
-    mtu_chunk_prefix(p, ck, sm.P, reinterpret_cast<uint32_t *>(sm.lst));
+    mtu_chunk_prefix(p, ck, sm.P, sm.ld);
+    uint8_t *gnx = p.nx + (size_t)c * kMtuChunk;
     mtu_chunk_next(sm.P, ck.cnt, [&](uint32_t i, uint16_t nxt) {
-        sm.lst[i] = nxt == kMtuEnd ? (uint16_t)i : nxt;
-        sm.dep[i] = nxt == kMtuEnd ? 0 : 1;
+        sm.ld[i] = nxt == kMtuEnd ? i << 16 : ((uint32_t)nxt << 16) | 1u;
+        gnx[i] = nxt == kMtuEnd ? 0 : (uint8_t)(nxt - i);   // for mtu_emit
     });
     __syncthreads();
     const uint32_t total = sm.P[ck.cnt - 1];
-    // pointer doubling: lst -> the last packet start of the chain, dep -> packets closed on it.
+    // pointer doubling: ld -> the last packet start of the chain and the packets closed on it.
     // A chain closes at most 2 * total / (cap + 1) + 1 packets (two consecutive closed packets
     // exceed the cap together), so that many jumps suffice.
     const uint32_t kb = min(ck.cnt, 2u * total / (uint32_t)(kMtuCap + 1) + 2u);
+    // In place, one barrier per round: a neighbour read mid-round has jumped at least as far as
+    // at the round's start, so after r rounds every jump spans >= 2^r starts (or ends the chain).
     for (uint32_t span = 1; !(SR_MTU_SKIP & 1) && span < kb; span <<= 1) {
-        uint16_t nl[kMtuPer], nd[kMtuPer];
 #pragma unroll
         for (int k = 0; k < kMtuPer; ++k) {
             const uint32_t i = (uint32_t)tid + (uint32_t)k * kMtuBlock;
             if (i < ck.cnt) {
-                const uint16_t l = sm.lst[i];
-                nl[k] = sm.lst[l];
-                nd[k] = (uint16_t)(sm.dep[i] + sm.dep[l]);
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kMtuPer; ++k) {
-            const uint32_t i = (uint32_t)tid + (uint32_t)k * kMtuBlock;
-            if (i < ck.cnt) {
-                sm.lst[i] = nl[k];
-                sm.dep[i] = nd[k];
+                const uint32_t v = sm.ld[i], w = sm.ld[v >> 16];
+                sm.ld[i] = (w & 0xFFFF0000u) | ((v + w) & 0xFFFFu);
             }
         }
         __syncthreads();
@@ -469,8 +461,8 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
             } else {
                 while (j > 0 && sm.P[j - 1] > lim) --j;
             }
-            const uint32_t l = sm.lst[j];
-            e = ((uint64_t)(1u + sm.dep[j]) << 32) | ((uint64_t)l << 16) | (total - (l ? sm.P[l - 1] : 0u));
+            const uint32_t v = sm.ld[j], l = v >> 16;
+            e = ((uint64_t)(1u + (v & 0xFFFFu)) << 32) | ((uint64_t)l << 16) | (total - (l ? sm.P[l - 1] : 0u));
         }
         row[x] = e;
     }
@@ -540,8 +532,13 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuLaunch L) {
     const MtuParams p = mtu_view(L, bi);
     const uint32_t c = blockIdx.x - L.b[bi].chunk0;
     if (!mtu_chunk_of(p, c, ck)) return;
-    mtu_chunk_prefix(p, ck, sm.P, reinterpret_cast<uint32_t *>(sm.nx));
-    mtu_chunk_next(sm.P, ck.cnt, [&](uint32_t i, uint16_t nxt) { sm.nx[i] = nxt == kMtuEnd ? 0 : (uint8_t)(nxt - i); });
+    {   // next(i) - i as mtu_table stored it: 16 bytes per thread
+        const uint4 *src = reinterpret_cast<const uint4 *>(p.nx + (size_t)c * kMtuChunk);
+        const uint32_t q = threadIdx.x;
+        const uint4 v = q * 16 < ck.cnt ? src[q] : make_uint4(0, 0, 0, 0);
+        mtu_chunk_prefix(p, ck, sm.P, reinterpret_cast<uint32_t *>(sm.nx));
+        reinterpret_cast<uint4 *>(sm.nx)[q] = v;
+    }
     __syncthreads();
     if (threadIdx.x >= 64) return;
     const uint32_t lane = threadIdx.x;

@@ -326,7 +326,9 @@ static int mtu_reserve(sr_ctx *c, uint32_t tiles, uint32_t chunks, uint32_t nb) 
         c->mtu_chunks = 0;
         // shard, entry, open, first descriptor per chunk
         if (hipMalloc(&c->d_mtu_chunks, 4 * (size_t)chunks * sizeof(uint32_t)) != hipSuccess) return -ENOMEM;
-        if (hipMalloc(&c->d_mtu_table, (size_t)chunks * kMtuX * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+        // the tables, then next(i) - i of every line of every chunk
+        if (hipMalloc(&c->d_mtu_table, (size_t)chunks * (kMtuX * sizeof(uint64_t) + kMtuChunk) + 16) != hipSuccess)
+            return -ENOMEM;
         c->mtu_chunks = chunks;
     }
     return 0;
@@ -376,6 +378,7 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     L.chunk_open = c->d_mtu_chunks + 2 * (size_t)chunks;
     L.chunk_pk = c->d_mtu_chunks + 3 * (size_t)chunks;
     L.table = c->d_mtu_table;
+    L.nx = reinterpret_cast<uint8_t *>(c->d_mtu_table + (((size_t)c->mtu_chunks * kMtuX + 1) & ~(size_t)1));
     const size_t sort_lds = (size_t)(nds + 1) * sizeof(uint32_t);
     hipLaunchKernelGGL(mtu_count_kernel, dim3(tiles), dim3(64), sort_lds, c->stream, L);
     hipLaunchKernelGGL(mtu_scan_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
