@@ -76,6 +76,8 @@ def parse(argv=None):
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-pack", action="store_true", help="skip the route + MTU packing leg")
+    ap.add_argument("--layout", default="auto", choices=["auto", "uniform", "segments"],
+                    help="route kernel lane layout (sr_set_layout; records identical either way)")
     ap.add_argument("--dry-ranks", action="store_true",
                     help="each rank prints its RANK / LOCAL_RANK / WORLD_SIZE and exits (launcher test; no GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
@@ -181,6 +183,8 @@ def main(argv=None):
     router = pkg.Router(shards, batch_bytes, device=local)
     router.set_alive(alive)
     router.set_stream(stream.cuda_stream)
+    router.set_layout({"auto": pkg.SR_LAYOUT_AUTO, "uniform": pkg.SR_LAYOUT_UNIFORM,
+                       "segments": pkg.SR_LAYOUT_SEGMENTS}[args.layout])
     in_ptr, out_ptr, cnt_ptr = d_in.data_ptr(), d_out.data_ptr(), d_cnt.data_ptr()
 
     def launch(gi):
@@ -201,6 +205,7 @@ def main(argv=None):
             with torch.cuda.graph(g, stream=stream):
                 launch(gi)
             graphs.append(g)
+        captured_layout = pkg.LAYOUT_NAMES.get(router.last_layout(), "?")
         # warm-up: W launches, and at least --min-warmup-ms of back-to-back launches
         t_w = time.perf_counter()
         w_done = 0
@@ -280,6 +285,7 @@ def main(argv=None):
                 "parallelism": f"dp{world} (independent datagram batches per GPU)",
                 "batches_per_launch": M,
                 "launch": f"hipGraph replay, one graph per launch of {M} batches, {ng} graphs alternating",
+                "lane_layout": f"{captured_layout} (sr_set_layout {args.layout})",
             },
             "gib_per_s": round(total_bytes / wall_max / 2**30, 3),
             "gpu_region_ms": round(region_max * 1e3, 4),

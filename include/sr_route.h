@@ -93,6 +93,25 @@ int sr_set_alive(sr_ctx *ctx, const uint64_t *alive_bitmap);
 /* Enqueue work on `stream` (a hipStream_t) instead of the context's own stream (NULL restores it). */
 int sr_set_stream(sr_ctx *ctx, void *stream);
 
+/* Lane layout of the route kernel. Timing only: the records are identical bit for bit.
+ *   SR_LAYOUT_UNIFORM  every line of a tile gets the same lane group, sized by the tile's mean
+ *                      line length (best for uniform lengths);
+ *   SR_LAYOUT_SEGMENTS a tile of mixed lengths gets one lane per 64-byte name segment, lines packed
+ *                      back to back (best when short and long lines share tiles);
+ *   SR_LAYOUT_AUTO     (default) segments while at least a quarter of the tiles of the last
+ *                      segment-layout launch took it (back below a tenth); uniform otherwise, with
+ *                      every 32nd launch outside stream capture (and the first) a segment-layout
+ *                      probe. A graph captured from the context keeps the layout of its capture.
+ * Returns 0 or -EINVAL. */
+#define SR_LAYOUT_AUTO 0
+#define SR_LAYOUT_UNIFORM 1
+#define SR_LAYOUT_SEGMENTS 2
+int sr_set_layout(sr_ctx *ctx, int layout);
+
+/* The layout the last route launch of the context used (SR_LAYOUT_UNIFORM or SR_LAYOUT_SEGMENTS;
+ * 0 before the first launch), or -EINVAL. */
+int sr_last_layout(const sr_ctx *ctx);
+
 /* Host-memory batch: copy `bytes` (concatenated framed datagrams; the last byte must be '\n'
  * unless nbytes == 0) to the device, classify every line, copy min(n, max_records) records (and,
  * if hashes != NULL, the 64-bit sdbm name hashes; 0 for invalid lines) back, and synchronise.

@@ -46,11 +46,14 @@ assert RECORD_DTYPE.itemsize == 8
 
 # every function the header declares (tests check the library exports exactly these)
 ABI_FUNCTIONS = (
-    "sr_frame_datagram", "sr_frame_datagrams", "sr_open", "sr_set_alive", "sr_set_stream",
+    "sr_frame_datagram", "sr_frame_datagrams", "sr_open", "sr_set_alive", "sr_set_stream", "sr_set_layout",
+    "sr_last_layout",
     "sr_route_batch", "sr_last_probed_dead", "sr_route_device", "sr_route_device_many", "sr_pack_by_owner",
     "sr_pack_many_by_owner", "sr_pack_packets", "sr_pack_packets_many", "sr_route_pack_batch", "sr_alloc_host", "sr_free_host", "sr_sync", "sr_close", "sr_version",
 )
 SR_MAX_PACK_DOWNSTREAMS = 4096
+SR_LAYOUT_AUTO, SR_LAYOUT_UNIFORM, SR_LAYOUT_SEGMENTS = 0, 1, 2
+LAYOUT_NAMES = {0: "none", 1: "uniform", 2: "segments"}
 PACKET_DTYPE = np.dtype([("first", "<u4"), ("nlines", "<u2"), ("shard", "<u2"), ("length", "<u2"),
                          ("carry", "<u2"), ("open", "<u4")])
 assert PACKET_DTYPE.itemsize == 16
@@ -129,6 +132,8 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_open": (ctypes.c_int, [ctypes.POINTER(vp), ctypes.c_int, ctypes.c_size_t, ctypes.c_uint32]),
         "sr_set_alive": (ctypes.c_int, [vp, u64p]),
         "sr_set_stream": (ctypes.c_int, [vp, vp]),
+        "sr_set_layout": (ctypes.c_int, [vp, ctypes.c_int]),
+        "sr_last_layout": (ctypes.c_int, [vp]),
         "sr_route_batch": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, c_size_p, vp]),
         "sr_last_probed_dead": (ctypes.c_int, [vp, u64p]),
         "sr_route_device": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp, vp]),
@@ -284,6 +289,15 @@ class Router:
         is not ordered with it."""
         _check(self._lib.sr_set_stream(self._h, ctypes.c_void_p(stream_handle or 0)), "sr_set_stream")
         self.stream_handle = int(stream_handle or 0)
+
+    def set_layout(self, layout: int) -> None:
+        """sr_set_layout: SR_LAYOUT_AUTO (default), SR_LAYOUT_UNIFORM or SR_LAYOUT_SEGMENTS (the
+        route kernel's lane layout; records are identical either way)."""
+        _check(self._lib.sr_set_layout(self._h, int(layout)), "sr_set_layout")
+
+    def last_layout(self) -> int:
+        """sr_last_layout: the lane layout of the context's last route launch (1 uniform, 2 segments)."""
+        return _check(self._lib.sr_last_layout(self._h), "sr_last_layout")
 
     def route(self, data: bytes | np.ndarray, max_records: int | None = None, want_hashes: bool = False):
         """sr_route_batch on host memory. Returns (records[n] structured array, hashes or None, n)."""

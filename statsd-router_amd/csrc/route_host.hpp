@@ -58,6 +58,15 @@ struct DeviceState {
     uint64_t *d_status = nullptr;
     uint64_t *d_bases = nullptr;
     PendingLine *d_pending = nullptr;
+    // lane layout of the route kernel (SR_LAYOUT_*): AUTO follows the segment statistics that
+    // KV_SEGMENTS launches publish into host-mapped memory (layout_out), probing now and then
+    int layout_mode = 0;
+    bool seg_on = false;             // AUTO: mixed-length traffic seen, KV_SEGMENTS launched
+    int last_layout = 0;             // the variant of the last launch (SR_LAYOUT_UNIFORM / _SEGMENTS)
+    uint32_t seen_seq = 0;
+    uint64_t launches = 0;
+    uint32_t *h_layout = nullptr;    // pinned, device-mapped: {sequence, tiles weighed, tiles segmented}
+    uint32_t *d_layout = nullptr;
 
     int init(size_t max_batch_bytes, uint32_t n_downstreams) {
         max_batch = max_batch_bytes;
@@ -75,6 +84,13 @@ struct DeviceState {
         if (hipMalloc(&d_bases, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
         if (hipMemset(d_bases, 0, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -EIO;
         if (hipMemset(d_ctl, 0, sizeof(Control)) != hipSuccess) return -EIO;
+        if (hipHostMalloc((void **)&h_layout, 4 * sizeof(uint32_t), hipHostMallocMapped | hipHostMallocCoherent) !=
+            hipSuccess) {
+            h_layout = nullptr;
+            return -ENOMEM;
+        }
+        memset(h_layout, 0, 4 * sizeof(uint32_t));
+        if (hipHostGetDevicePointer((void **)&d_layout, h_layout, 0) != hipSuccess) return -EIO;
 
         if (hipMemset(d_status, 0, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -EIO;
         std::vector<Magic> mg(n_downstreams + 1);
@@ -110,6 +126,9 @@ struct DeviceState {
         (void)hipFree(d_status);
         (void)hipFree(d_bases);
         (void)hipFree(d_pending);
+        if (h_layout) (void)hipHostFree(h_layout);
+        h_layout = nullptr;
+        d_layout = nullptr;
         free(h_alive);
         d_alive = nullptr;
         d_magic = nullptr;
@@ -161,7 +180,36 @@ struct DeviceState {
         p.bases = d_bases;
         p.pending = d_pending;
         p.dbg = nullptr;
+        p.layout_out = d_layout;
         return p;
+    }
+
+    // The route kernel variant for the next launch. AUTO: switch to KV_SEGMENTS when at least a
+    // quarter of the tiles a KV_SEGMENTS launch weighed took the segment layout, back below a
+    // tenth; while uniform, every 32nd launch outside stream capture is a KV_SEGMENTS probe (the
+    // first launch is one). Records are identical either way; only the time differs.
+    bool choose_segments(hipStream_t stream) {
+        bool seg;
+        if (layout_mode == SR_LAYOUT_UNIFORM) {
+            seg = false;
+        } else if (layout_mode == SR_LAYOUT_SEGMENTS) {
+            seg = true;
+        } else {
+            const uint32_t seq = __atomic_load_n(&h_layout[0], __ATOMIC_ACQUIRE);
+            if (seq != seen_seq) {
+                seen_seq = seq;
+                const uint32_t weighed = __atomic_load_n(&h_layout[1], __ATOMIC_RELAXED);
+                const uint32_t segmented = __atomic_load_n(&h_layout[2], __ATOMIC_RELAXED);
+                if (!seg_on && 4ull * segmented >= weighed) seg_on = true;
+                else if (seg_on && 10ull * segmented < weighed) seg_on = false;
+            }
+            hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+            const bool capturing = hipStreamIsCapturing(stream, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+            seg = seg_on || (!capturing && launches % 32 == 0);
+            if (!capturing) ++launches;
+        }
+        last_layout = seg ? SR_LAYOUT_SEGMENTS : SR_LAYOUT_UNIFORM;
+        return seg;
     }
 
     // one-batch launch parameters

@@ -77,11 +77,13 @@ enum : unsigned {
                              // the pipelined scanner publishes ahead of need)
     ABL_AGENT_GRANULES = 262144u,  // every count / base granule stored sc1 (round-1 v0.5), whatever the XCDs
     ABL_SCAN_SERIAL = 524288u,  // round-1 v0.6 scanner: 256 granules per round trip, one poll in flight
-    ABL_MIXED_LANES = 1048576u,  // per-line lane groups for tiles of mixed line lengths (opt-in: C5 -13 %,
-                                 // but its classification costs C2 / C4 2-5 % in registers)
     ABL_NO_MID_BASE = 2097152u,  // no base read part-way through the hash (round-1 v0.8)
     ABL_OLD_HASH = 1024u,   // round-1 v0.5 per-segment sdbm (v_alignbyte reads, compiler-extracted bytes)
 };
+
+// Product kernel variants (same records, bit for bit): KV_SEGMENTS lays a tile of mixed line
+// lengths out one lane per 64-byte name segment (route_host.hpp picks the variant per launch).
+enum : unsigned { KV_UNIFORM = 0u, KV_SEGMENTS = 4194304u };
 
 constexpr uint64_t ipow(uint64_t b, unsigned e) {
     uint64_t r = 1;
@@ -125,6 +127,9 @@ struct Control {
     uint32_t pad0[29];
     uint32_t done[8][32];
     uint64_t scan_xcc[32];   // per batch: the XCD its scanner runs on (kFlagXcc granule)
+    uint32_t layout[8][32];  // KV_SEGMENTS launches, sharded: [0] tiles that weighed the segment
+                             // layout, [1] tiles it saves two or more rounds (published per launch
+                             // by the last block)
 };
 
 // One batch of a launch. A launch routes up to kMaxBatches independent batches: tiles
@@ -164,6 +169,8 @@ struct RouteParams {
     uint64_t *bases;         // per-tile first-record granules {epoch, flag, base} (written by the scanner)
     PendingLine *pending;
     uint64_t *dbg;           // ABL_STAMPS builds only: 16 timestamp slots per tile
+    uint32_t *layout_out;    // host-mapped {sequence, tiles weighed, tiles segmented} of the last
+                             // KV_SEGMENTS launch (null: not published)
     // per XCD class c, its batches in tile order: (class-local end tile << 6) | batch index;
     // ~0u after the last (one scalar load finds a tile's batch)
     uint32_t cls_tab[8][kPerClass];
@@ -547,9 +554,14 @@ struct SmemT {
     int32_t lend[kWin + 1];          // per staged line: tile position of its '\n'; slot 0 = previous
     int32_t lcol[kWin + 1];          // per staged line: first ':' in the tile part (kNone if none)
     uint32_t wave_cnt[kWaves];
-    uint32_t ccnt[kWaves][6];        // per wave: lines of the window per lane class
-    uint32_t ctab[6];                // per lane class: (first lane << 16) | first sorted slot
-    uint8_t lorder[kWin];            // the window's lines sorted by lane class, largest first
+    // segment layout of a window (tiles of mixed lengths): lanes wanted per wave, line starts as a
+    // lane bitmap, per 64-lane word the line covering its first lane ((start << 16) | line) and the
+    // part of the line a word passes on to the next
+    static constexpr int kSegWords = ((kTileB + kHalo) / 64 + kWin) / 64 + 4;
+    uint32_t seg_w[kWaves][2];
+    uint64_t seg_mask[kSegWords];
+    uint32_t seg_first[kSegWords];
+    uint64_t seg_carry[kSegWords];
     uint32_t wave_scan[kWaves][4];   // per wave, inclusive at its last lane: '\n' count, latest '\n' lane, colon key
     uint64_t kp_lo[kPowLo];          // K^i
     uint64_t kp_hi[kPowHi];          // K^(64 i)
@@ -990,9 +1002,17 @@ __device__ void arrive(const RouteParams &p, uint32_t blk, uint32_t epoch) {
         if (n >= p.total_blocks) break;
         __builtin_amdgcn_s_sleep(2);
     }
+    uint32_t weighed = 0, segmented = 0;
 #pragma unroll
     for (int s8 = 0; s8 < 8; ++s8) {
         __hip_atomic_store(&p.ctl->done[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        weighed += __hip_atomic_exchange(&p.ctl->layout[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        segmented += __hip_atomic_exchange(&p.ctl->layout[s8][1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (weighed && p.layout_out) {   // the host's layout choice reads these (route_host.hpp)
+        __hip_atomic_store(&p.layout_out[1], weighed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&p.layout_out[2], segmented, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&p.layout_out[0], epoch + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __hip_atomic_store(&p.ctl->epoch, epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1133,7 +1153,6 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
     } else {
     // ---- per lane: '\n' / ':' masks of its 64 contiguous bytes, segmented line-state scan -------
     const int o = tid * kLaneBytes;   // tile position of the lane's first byte (nlm / clm bit i: byte o + i)
-    const int ncnt = __popcll(nlm);
     // Line state before each lane's chunk, by three u32 wave scans (DPP) and a prefix over the
     // earlier waves: the number of '\n' before it, and the first ':' of the line open at its start.
     //  * the colon candidate of a chunk is its first ':' after its last '\n' (or its first ':' if it
@@ -1141,36 +1160,41 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
     //    from the latest chunk with a '\n' on;
     //  * key = ((BLOCK - L) << 17) | candidate, L = 1 + latest thread with a '\n' up to here (0: none
     //    in this wave), so a min-scan of keys takes the smallest candidate of the latest segment.
-    uint32_t cand;
-    {
-        uint64_t cm = clm;
-        if (nlm) {
-            const int lastb = 63 - __clzll(nlm);
-            cm = lastb == 63 ? 0ull : (clm & (~0ull << (lastb + 1)));
+    auto lane_cand = [&](uint64_t nl, uint64_t cl) -> uint32_t {
+        uint64_t cm = cl;
+        if (nl) {
+            const int lastb = 63 - __clzll(nl);
+            cm = lastb == 63 ? 0ull : (cl & (~0ull << (lastb + 1)));
         }
-        cand = cm ? (uint32_t)(o + __builtin_ctzll(cm)) : (uint32_t)kNone;
-    }
+        return cm ? (uint32_t)(o + __builtin_ctzll(cm)) : (uint32_t)kNone;
+    };
+    // the lane's first line and the first ':' of the line open at its start, from the inclusive
+    // wave scans and the earlier waves' totals (sm.wave_scan)
+    auto lane_state = [&](uint32_t cin, uint32_t lin, uint32_t kin, int &lf, int &ofc) {
+        uint32_t p_cnt = 0, p_col = (uint32_t)kNone;   // the earlier waves: '\n' count, open line's first ':'
+#pragma unroll
+        for (int w = 0; w < kWaves - 1; ++w) {
+            if (w < wave) {
+                const uint4 ws = *(const uint4 *)&sm.wave_scan[w][0];
+                p_cnt += ws.x;
+                const uint32_t wc = ws.z & 0x1FFFFu;
+                p_col = ws.y ? wc : min(p_col, wc);
+            }
+        }
+        // exclusive state of this lane: the inclusive state of the lane below, on top of the prefix
+        const uint32_t c_ex = wave_shr1_32(cin, 0u);
+        const uint32_t l_ex = wave_shr1_32(lin, 0u);
+        const uint32_t k_ex = wave_shr1_32(kin, 0xFFFFFFFFu) & 0x1FFFFu;
+        lf = (int)(p_cnt + c_ex);                       // tile-local index of lane's 1st line
+        ofc = (int)(l_ex ? k_ex : min(p_col, k_ex));    // first ':' (in the tile) of the open line
+    };
     const uint32_t l_in = wave_incl_max32(nlm ? (uint32_t)tid + 1u : 0u);
-    const uint32_t k_in = wave_incl_min32(((uint32_t)(BLOCK - (int)l_in) << 17) | cand);
+    const uint32_t k_in = wave_incl_min32(((uint32_t)(BLOCK - (int)l_in) << 17) | lane_cand(nlm, clm));
     if (lane == 63) *(uint4 *)&sm.wave_scan[wave][0] = make_uint4(c_in, l_in, k_in, 0u);
     wg_barrier();
     stamp<ABL>(p, tid, g, 2);
-    uint32_t p_cnt = 0, p_col = (uint32_t)kNone;   // the earlier waves: '\n' count, open line's first ':'
-#pragma unroll
-    for (int w = 0; w < kWaves - 1; ++w) {
-        if (w < wave) {
-            const uint4 ws = *(const uint4 *)&sm.wave_scan[w][0];
-            p_cnt += ws.x;
-            const uint32_t wc = ws.z & 0x1FFFFu;
-            p_col = ws.y ? wc : min(p_col, wc);
-        }
-    }
-    // exclusive state of this lane: the inclusive state of the lane below, on top of the prefix
-    const uint32_t c_ex = wave_shr1_32(c_in, 0u);
-    const uint32_t l_ex = wave_shr1_32(l_in, 0u);
-    const uint32_t k_ex = wave_shr1_32(k_in, 0xFFFFFFFFu) & 0x1FFFFu;
-    const int lane_first = (int)(p_cnt + c_ex);                       // tile-local index of lane's 1st line
-    const int open_fc = (int)(l_ex ? k_ex : min(p_col, k_ex));        // first ':' (in the tile) of the open line
+    int lane_first, open_fc;
+    lane_state(c_in, l_in, k_in, lane_first, open_fc);
 
     // ---- last wave: where the line that straddles into the tile starts, its first ':' ----------
     if (wave == kPreWave) {
@@ -1241,25 +1265,23 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
     }
 
     // ---- per line: windows of kWin tile-local lines ------------------------------------------
-    if (tid == 0) sm.lend[0] = 0;
-    uint32_t base = (ABL & ABL_FAKE_BASE) ? t * tile_count : 0u;   // first record index of the tile
-    bool have_base = (ABL & (ABL_NO_LOOKBACK | ABL_NO_LINES | ABL_FAKE_BASE)) != 0;
-    for (int wbase = 0; wbase < (int)tile_count; wbase += kWin) {
-        // (1) stage (e, c) of the lane's lines that fall into this window
-        if (nlm && lane_first + ncnt > wbase && lane_first < wbase + kWin) {
-            uint64_t m = nlm;
-            int idx = lane_first;
+    // (e, c) of the lane's lines that fall into window [wbase, wbase + kWin) into sm.lend / lcol
+    auto stage = [&](int wbase, uint64_t nl, uint64_t cl, int lf, int ofc) {
+        const int nc = __popcll(nl);
+        if (nl && lf + nc > wbase && lf < wbase + kWin) {
+            uint64_t m = nl;
+            int idx = lf;
             int prevb = -1;
             while (m) {
                 const int b = __builtin_ctzll(m);
                 m &= m - 1;
                 int c;
-                if (prevb < 0 && open_fc != kNone) {
-                    c = open_fc;
+                if (prevb < 0 && ofc != kNone) {
+                    c = ofc;
                 } else {
                     const uint64_t below = b == 0 ? 0ull : (~0ull >> (64 - b));
                     const uint64_t above = ~0ull << (prevb + 1);
-                    const uint64_t cm = clm & below & above;
+                    const uint64_t cm = cl & below & above;
                     c = cm ? o + __builtin_ctzll(cm) : kNone;
                 }
                 if (idx >= wbase && idx < wbase + kWin) {
@@ -1270,6 +1292,14 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 prevb = b;
             }
         }
+    };
+    if (tid == 0) sm.lend[0] = 0;
+    uint32_t base = (ABL & ABL_FAKE_BASE) ? t * tile_count : 0u;   // first record index of the tile
+    bool have_base = (ABL & (ABL_NO_LOOKBACK | ABL_NO_LINES | ABL_FAKE_BASE)) != 0;
+    // Window 0 is staged from the masks in registers; later windows (tiles of more than kWin lines)
+    // recompute them from the LDS image, so that no mask or line state stays live through the hash.
+    if (tile_count > 0) stage(0, nlm, clm, lane_first, open_fc);
+    for (int wbase = 0; wbase < (int)tile_count;) {
         wg_barrier();
         if (wbase == 0) stamp<ABL>(p, tid, g, 4);
         // the tile's record base is read when the first record is written (ABL_EARLY_BASE: also
@@ -1285,6 +1315,34 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
             // (G * 64 < kTileB / tile_count, without the division)
             int G = 1;
             while (G < 32 && (G * 64 + 1) * (int)tile_count <= kTileB) G <<= 1;
+            // the line's record: verdict, shard, record base (normally long published), write
+            auto finish = [&](int j, int s, int len, bool len_ok, bool fmt_ok, uint64_t h) {
+                uint32_t route;
+                if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
+                else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
+                else route = probe_shard(h, p);                                                    // :145
+                sr_record r;
+                r.offset = (uint32_t)(T0 + s);
+                r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
+                r.route = (uint16_t)route;
+                if (!have_base) {
+                    stamp<ABL>(p, tid, g, 3);
+                    base = granule_ok(st_early, epoch & 0x3FFFFFFFu, kFlagBase)
+                               ? (uint32_t)st_early
+                               : wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
+                    stamp<ABL>(p, tid, g, 7);
+                    have_base = true;
+                }
+                const uint32_t rec = base + (uint32_t)j;
+                if (rec < bd.max_records) {
+                    if (route == kRoutePending) {
+                        const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
+                        if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
+                    }
+                    bd.recs[rec] = r;
+                    if (bd.hashes) bd.hashes[rec] = h;
+                }
+            };
             // One line's work: bounds, verdict, sdbm (lane gi of the line's Gl lanes takes the
             // 64-byte segments gi, gi + Gl, ...), shard, record. Gw: the wave-uniform bound of
             // the lane groups (groups are aligned to their size, so xor partners below Gl stay
@@ -1315,41 +1373,23 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     const uint64_t v = shfl_xor64(h, d);
                     if (d < Gl) h += v;
                 }
-                if (act && gi == 0) {
-                    uint32_t route;
-                    if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
-                    else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
-                    else route = probe_shard(h, p);                                                    // :145
-                    sr_record r;
-                    r.offset = (uint32_t)(T0 + s);
-                    r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
-                    r.route = (uint16_t)route;
-                    if (!have_base) {   // needed only now, after the hash: normally long published
-                        stamp<ABL>(p, tid, g, 3);
-                        base = granule_ok(st_early, epoch & 0x3FFFFFFFu, kFlagBase)
-                                   ? (uint32_t)st_early
-                                   : wait_base(base_slot, epoch, rsrc, (uint32_t)T0);
-                        stamp<ABL>(p, tid, g, 7);
-                        have_base = true;
-                    }
-                    const uint32_t rec = base + (uint32_t)j;
-                    if (rec < bd.max_records) {
-                        if (route == kRoutePending) {
-                            const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
-                            if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
-                        }
-                        bd.recs[rec] = r;
-                        if (bd.hashes) bd.hashes[rec] = h;
-                    }
-                }
+                if (act && gi == 0) finish(j, s, len, len_ok, fmt_ok, h);
             };
-            // Lane classes: thread tid describes line tid of the window; class k = log2 of the
-            // lanes its hash wants (2^k >= its 64-byte segments, at most 32).
-            int ncl = 0;
-            uint32_t TL = 0, Gmax = 1;   // lanes all lines want; the largest class
-            // only tiles of long lines on average (G > 1) can gain; C2-like tiles skip this
-            const bool classify = (ABL & ABL_MIXED_LANES) && G > 1;
-            if (classify) {
+            // Lanes per line. A tile whose longest name fits its G lanes in one pass (uniform
+            // lengths: C2, C4) keeps one G-lane group per line (G = 1: no pre-pass at all). A tile
+            // of mixed lengths (C5: a 64-byte line next to 1024-byte ones) gets one lane per
+            // 64-byte name segment instead, the lines packed back to back over the lanes: no idle
+            // lanes, one segment per lane.
+            bool segs = false, U2 = false;   // segment layout; lane units of two segments
+            bool gain2 = false;              // the segment layout saves two or more rounds
+            uint32_t TL = 0;                  // lanes the segment layout needs
+            // (the segment variant decides in a tile's last window, after which the lane masks and
+            // line states of later windows are dead)
+            const bool last_win = wbase + kWin >= (int)tile_count;
+            if ((ABL & KV_SEGMENTS) && last_win && G > 1) {
+                // per line: 64-byte name segments, and lane units of one or two segments (two
+                // when one-segment units would take a second round of lanes)
+                uint32_t want = 0, nsg = 0;
                 if (tid < nwin) {
                     const int jj = tid, j = wbase + jj;
                     const int e = sm.lend[jj + 1];
@@ -1357,102 +1397,133 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     if (j == 0 && c_pre != kNone) c = c_pre;
                     const int s = (j == 0) ? s_pre : sm.lend[jj] + 1;
                     const int len = e - s + 1;
-                    if (len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH && c != kNone && c < e) {
-                        const int nseg = (c - s + 63) >> 6;
-                        ncl = nseg <= 1 ? 0 : min(5, 32 - __builtin_clz((unsigned)(nseg - 1)));
-                    }
+                    if (len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH && c != kNone && c < e)
+                        nsg = (uint32_t)(c - s + 63) >> 6;
+                    want = max(1u, nsg) | (max(1u, (nsg + 1) >> 1) << 16);
                 }
-                const uint32_t want = tid < nwin ? 1u << ncl : 0u;
-                const uint32_t wsum = wave_add32(want);
-                const uint32_t wmax = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max32(want), 63);
-                if (lane == 0) {
-                    sm.ccnt[wave][0] = wsum;
-                    sm.ccnt[wave][1] = wmax;
+                const uint32_t incl = wave_incl_add32(want);
+                const uint32_t wmx = wave_incl_max32(nsg);
+                if (lane == 63) {
+                    sm.seg_w[wave][0] = incl;
+                    sm.seg_w[wave][1] = wmx;
                 }
+                if (tid < 2 * S::kSegWords) reinterpret_cast<uint32_t *>(sm.seg_mask)[tid] = 0u;
                 wg_barrier();
-                uint32_t cls_or = 0;
+                uint32_t pre = 0, mx = 0, tot = 0;
 #pragma unroll
                 for (int w = 0; w < kWaves; ++w) {
-                    TL += sm.ccnt[w][0];
-                    cls_or = max(cls_or, sm.ccnt[w][1]);
+                    const uint32_t v = sm.seg_w[w][0];
+                    tot += v;
+                    pre += w < wave ? v : 0u;
+                    mx = max(mx, sm.seg_w[w][1]);
                 }
-                TL = __builtin_amdgcn_readfirstlane(TL);
-                Gmax = max(1u, (uint32_t)__builtin_amdgcn_readfirstlane(cls_or));
+                tot = __builtin_amdgcn_readfirstlane(tot);
+                U2 = (tot & 0xFFFFu) > (uint32_t)BLOCK;
+                const int sh = U2 ? 16 : 0;
+                TL = (tot >> sh) & 0xFFFFu;
+                // rounds of lanes times segments per lane, either way; the statistics for the
+                // host's choice of kernel count only the tiles that gain two or more
+                const uint32_t mxs = (uint32_t)__builtin_amdgcn_readfirstlane(mx);
+                const int cost_u = ((nwin * G + BLOCK - 1) / BLOCK) * (int)((mxs + (uint32_t)G - 1) / (uint32_t)G);
+                const int cost_s = (((int)TL + BLOCK - 1) / BLOCK) * (U2 ? 2 : 1);
+                segs = cost_s < cost_u;
+                gain2 = cost_s + 2 <= cost_u;
+                if (segs) {
+                    // line starts as bits of a lane bitmap; per 64-lane word, the line covering
+                    // its first lane and where that line starts
+                    if (tid < nwin) {
+                        const uint32_t wn = (want >> sh) & 0xFFFFu;
+                        const uint32_t st = ((pre + incl - want) >> sh) & 0xFFFFu;
+                        atomicOr(&sm.seg_mask[st >> 6], 1ull << (st & 63));
+                        const uint32_t m = (st + 63) & ~63u;
+                        if (m < st + wn) sm.seg_first[m >> 6] = (st << 16) | (uint32_t)tid;
+                    }
+                    wg_barrier();
+                }
             }
-            // Rounds either way: the tile-wide G (every line G lanes; a longer line's lanes walk
-            // several segments) or one lane group per line sized to the line (groups packed in
-            // descending size). The latter wins on mixed lengths (C5).
-            const int cost_tile = ((nwin * G + BLOCK - 1) / BLOCK) * (((int)Gmax + G - 1) / G);
-            const int cost_mixed = ((int)TL + BLOCK - 1) / BLOCK + 1;
-            const bool mixed = classify && cost_mixed <= cost_tile;
-            if (mixed) {
-                // counting sort of the window's lines by class, largest first, into sm.lorder;
-                // sm.ctab[k] = (first lane of class k << 16) | (first sorted slot of class k)
-                uint32_t rank = 0;
-                wg_barrier();   // every wave has read the totals before ccnt is reused
-#pragma unroll
-                for (int k = 0; k < 6; ++k) {
-                    const uint64_t m = __ballot(tid < nwin && ncl == k);
-                    if (lane == 0) sm.ccnt[wave][k] = (uint32_t)__popcll(m);
-                    if (ncl == k) rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if ((ABL & KV_SEGMENTS) && last_win && tid == 0) {   // the layout statistics (arrive)
+                __hip_atomic_fetch_add(&p.ctl->layout[g & 7u][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (gain2)
+                    __hip_atomic_fetch_add(&p.ctl->layout[g & 7u][1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (!segs) {
+                for (int r0 = 0; r0 < nwin * G; r0 += BLOCK) {
+                    const uint32_t x = (uint32_t)(r0 + tid);
+                    const int jj = (int)(x >> __builtin_ctz((unsigned)G));
+                    line(jj, jj < nwin, (int)(x & (uint32_t)(G - 1)), G, G);
                 }
-                wg_barrier();
-                if (tid == 0) {
-                    uint32_t lo = 0, first = 0;
-                    for (int k = 5; k >= 0; --k) {
-                        uint32_t n = 0;
-                        for (int w = 0; w < kWaves; ++w) n += sm.ccnt[w][k];
-                        sm.ctab[k] = (lo << 16) | first;
-                        lo += n << k;
-                        first += n;
+            } else {
+                for (int r0 = 0; r0 < (int)TL; r0 += BLOCK) {
+                    const uint32_t x = (uint32_t)(r0 + tid);
+                    const uint32_t k = x >> 6;   // the lane word: wave-uniform
+                    const bool act = x < TL;
+                    const uint64_t mask = readlane64(act ? sm.seg_mask[k] : 0ull, 0);
+                    const uint32_t fst = (uint32_t)__builtin_amdgcn_readfirstlane(act ? sm.seg_first[k] : 0u);
+                    const uint64_t below = mask & (~0ull >> (63 - lane));
+                    const int hb = below ? 63 - __clzll(below) : -1;   // head lane of my line here
+                    const int jj = (int)(fst & 0xFFFFu) + __popcll(below) - (int)(mask & 1ull);
+                    const int sg = below ? lane - hb : (int)(x - (fst >> 16));   // my segment of the line
+                    const int j = wbase + jj;
+                    const int e = act ? sm.lend[jj + 1] : 0;
+                    int c = act ? sm.lcol[jj + 1] : kNone;
+                    if (j == 0 && c_pre != kNone) c = c_pre;
+                    const int s = (j == 0) ? s_pre : (act ? sm.lend[jj] + 1 : 0);
+                    const int len = e - s + 1;
+                    const bool len_ok = len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH;   // :180
+                    const bool fmt_ok = c != kNone && c < e;                                                // :140
+                    const int n = c - s;
+                    const int nseg = (act && len_ok && fmt_ok) ? (n + 63) >> 6 : 0;   // 0: an empty name
+                    const int glast = max(U2 ? (nseg + 1) >> 1 : nseg, 1) - 1;          // the line's last lane
+                    uint64_t hs = 0;
+                    for (int kk = 0; kk <= (int)U2; ++kk) {   // my unit: segments (U2 + 1) sg + kk
+                        const int kq = (U2 ? 2 * sg : sg) + kk;
+                        if (kq < nseg) {
+                            const int a = s + 64 * kq, nn = min(64, n - 64 * kq);
+                            const bool mid = !have_base && kq == nseg - 1;
+                            uint64_t hq = sdbm_img(sm, a + kHalo, nn, mid ? base_slot : nullptr, &st_early);
+                            if (kq + 1 < nseg) hq *= kpow_n(sm, c - a - nn);
+                            hs += hq;
+                        }
+                    }
+                    // a line's sum from the inclusive wave scan: S(x) - S(head - 1), or S(x) plus
+                    // the line's part in the previous word (a line spans at most 23 lanes)
+                    const uint64_t S = wave_scan64(hs, 0ull, [](uint64_t l, uint64_t r) { return l + r; });
+                    const int src = hb > 0 ? hb - 1 : 0;
+                    const uint64_t Sb = ((uint64_t)(uint32_t)__shfl((int)(S >> 32), src, 64) << 32) |
+                                        (uint32_t)__shfl((int)(uint32_t)S, src, 64);
+                    const uint64_t part = hb > 0 ? S - Sb : S;
+                    if (lane == 63 && act && sg < glast) sm.seg_carry[k] = part;   // continues in word k + 1
+                    wg_barrier();
+                    if (act && sg == glast) {
+                        const uint64_t h = below ? part : part + sm.seg_carry[k - 1];
+                        finish(j, s, len, len_ok, fmt_ok, h);
                     }
                 }
-                wg_barrier();
-                if (tid < nwin) {
-                    uint32_t pos = (sm.ctab[ncl] & 0xFFFFu) + rank;
-                    for (int w = 0; w < wave; ++w) pos += sm.ccnt[w][ncl];
-                    sm.lorder[pos] = (uint8_t)tid;
-                }
-                wg_barrier();
-            }
-            // wave-uniform rounds over the lanes the lines want (the base resolution needs every
-            // lane of the wave): tile-wide G, or the sorted per-line groups
-            const int lanes_total = mixed ? (int)TL : nwin * G;
-            const int Gw = mixed ? (int)Gmax : G;
-            for (int r0 = 0; r0 < lanes_total; r0 += BLOCK) {
-                const uint32_t x = (uint32_t)(r0 + tid);
-                int jj, gi, Gl;
-                bool act;
-                if (!mixed) {
-                    jj = (int)(x >> __builtin_ctz((unsigned)G));
-                    gi = (int)(x & (uint32_t)(G - 1));
-                    Gl = G;
-                    act = jj < nwin;
-                } else {
-                    // the class whose lane range [lo_k, lo_(k-1)) holds x (class 5 starts at lane 0)
-                    int k = -1;
-#pragma unroll
-                    for (int kk = 5; kk >= 0; --kk) {
-                        const uint32_t lo = sm.ctab[kk] >> 16;
-                        const uint32_t hi = kk ? (sm.ctab[kk - 1] >> 16) : TL;
-                        if (k < 0 && x >= lo && x < hi) k = kk;
-                    }
-                    act = k >= 0;
-                    const int kc = act ? k : 0;
-                    const uint32_t t = sm.ctab[kc];
-                    const uint32_t off = act ? x - (t >> 16) : 0u;
-                    jj = act ? (int)sm.lorder[(t & 0xFFFFu) + (off >> kc)] : 0;
-                    gi = (int)(off & ((1u << kc) - 1u));
-                    Gl = 1 << kc;
-                }
-                line(jj, act, gi, Gl, Gw);
             }
         }
 
         wg_barrier();
         if (wbase == 0) stamp<ABL>(p, tid, g, 5);
-        if (tid == 0) sm.lend[0] = sm.lend[min(kWin, (int)tile_count - wbase)];
+        if (wbase + kWin >= (int)tile_count) break;
+        if (tid == 0) sm.lend[0] = sm.lend[kWin];
         wg_barrier();
+        wbase += kWin;
+        {   // the lane's masks and line state again, from the image and the wave totals in LDS
+            const uint32_t *const row = &sm.img[(kHalo / 64 + tid) * 17];
+            uint32_t m[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) m[k] = nl_colon_mask16(make_uint4(row[4 * k], row[4 * k + 1], row[4 * k + 2], row[4 * k + 3]));
+            const uint64_t nl = ((uint64_t)__builtin_amdgcn_perm(m[3], m[2], 0x05040100u) << 32) |
+                                __builtin_amdgcn_perm(m[1], m[0], 0x05040100u);
+            const uint64_t cl = ((uint64_t)__builtin_amdgcn_perm(m[3], m[2], 0x07060302u) << 32) |
+                                __builtin_amdgcn_perm(m[1], m[0], 0x07060302u);
+            const uint32_t cin = wave_incl_add32((uint32_t)__popcll(nl));
+            const uint32_t lin = wave_incl_max32(nl ? (uint32_t)tid + 1u : 0u);
+            const uint32_t kin = wave_incl_min32(((uint32_t)(BLOCK - (int)lin) << 17) | lane_cand(nl, cl));
+            int lf, ofc;
+            lane_state(cin, lin, kin, lf, ofc);
+            stage(wbase, nl, cl, lf, ofc);
+        }
     }
     }
     stamp<ABL>(p, tid, g, 6);

@@ -57,8 +57,16 @@ static void free_ptr(void *p) { (void)hipFree(p); }
 // The product launches exactly one instantiation, ABL_NONE. Ablation variants (records wrong by
 // design in some of them) exist only in builds made with -DSR_ABLATION_VARIANTS (`make VARIANTS=1`,
 // developer A/B runs; never the shipped library): SR_VARIANT in the environment then selects one.
+// The product launches KV_UNIFORM or KV_SEGMENTS (identical records; DeviceState::choose_segments
+// picks by the lane-layout policy). Ablation variants (records wrong by design in some of them)
+// exist only in builds made with -DSR_ABLATION_VARIANTS (`make VARIANTS=1`, developer A/B runs;
+// never the shipped library): SR_VARIANT in the environment then selects one.
+static int launch_product(DeviceState &ds, const RouteParams &p, hipStream_t stream) {
+    if (ds.choose_segments(stream)) return launch_route<kBlock, KV_SEGMENTS>(ds, p, stream);
+    return launch_route<kBlock, KV_UNIFORM>(ds, p, stream);
+}
 #ifdef SR_ABLATION_VARIANTS
-static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream_t stream) {
+static int launch_variant(DeviceState &ds, const RouteParams &p, hipStream_t stream) {
     static const int v = [] {
         const char *e = getenv("SR_VARIANT");
         if (!e || !*e) return 0;
@@ -74,12 +82,12 @@ static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream
     case 7: return launch_route<kBlock, ABL_FAKE_BASE>(ds, p, stream);
     case 8: return launch_route<kBlock, ABL_NO_HASH>(ds, p, stream);
     case 9: return launch_route<kBlock, ABL_NO_LINES>(ds, p, stream);
-    default: return launch_route<kBlock, ABL_NONE>(ds, p, stream);
+    default: return launch_product(ds, p, stream);
     }
 }
 #else
-static int launch_variant(const DeviceState &ds, const RouteParams &p, hipStream_t stream) {
-    return launch_route<kBlock, ABL_NONE>(ds, p, stream);
+static int launch_variant(DeviceState &ds, const RouteParams &p, hipStream_t stream) {
+    return launch_product(ds, p, stream);
 }
 #endif
 
@@ -183,6 +191,14 @@ int sr_set_stream(sr_ctx *c, void *stream) {
     c->stream = stream ? (hipStream_t)stream : c->own_stream;
     return 0;
 }
+
+int sr_set_layout(sr_ctx *c, int layout) {
+    if (!c || layout < SR_LAYOUT_AUTO || layout > SR_LAYOUT_SEGMENTS) return -EINVAL;
+    c->ds.layout_mode = layout;
+    return 0;
+}
+
+int sr_last_layout(const sr_ctx *c) { return c ? c->ds.last_layout : -EINVAL; }
 
 int sr_sync(sr_ctx *c) {
     if (!c) return -EINVAL;

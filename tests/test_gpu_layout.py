@@ -1,0 +1,96 @@
+"""The route kernel's two lane layouts (sr_set_layout): KV_UNIFORM (one lane group per line, sized by
+the tile's mean line length) and KV_SEGMENTS (one lane per 64-byte name segment in tiles of mixed
+lengths) must give the same records and hashes bit for bit, both equal to the oracle; AUTO follows
+the segment statistics the kernel publishes. Needs an MI355X: `pytest -m gpu`."""
+from __future__ import annotations
+
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import load_digests
+from test_gpu_parity import _assert_same, _hostile_stream, _lines_stream
+
+pytestmark = pytest.mark.gpu
+
+UNIFORM, SEGMENTS = 1, 2
+
+
+def _streams(pkg):
+    rng = np.random.default_rng(5)
+    yield "c5_mixed_1MiB", pkg.gen_stream(1 << 20, [64, 256, 1024], seed=0x5EED0005).data
+    yield "c2_64B_1MiB", pkg.gen_stream(1 << 20, [64], seed=0x5EED0002).data
+    yield "c3_invalid", pkg.gen_stream(1 << 20, [256], seed=3, p_invalid=0.1).data
+    yield "lengths_1_to_1600", _lines_stream(rng.integers(1, 1600, 3000).tolist(), seed=9)
+    yield "short_and_1449", _lines_stream([6, 1449, 7, 64, 1449, 1449, 9, 200] * 400, seed=10)
+    yield "empty_names", b"".join([b":1|c\n", b"x" * 900 + b":v\n", b"ab:\n", b":\n"] * 500)
+    yield "dense_newlines", b"\n" * 40_000 + _lines_stream([6] * 9000, seed=3) + b"\n" * 100
+    yield "hostile", pkg.frame_datagrams(_hostile_stream(7, 300_000))
+
+
+@pytest.mark.parametrize("n,dead", [(4, 0), (64, 0), (64, 20)])
+def test_layouts_match_oracle(pkg, oracle, n, dead):
+    alive = [0 if i < dead else 1 for i in range(n)]
+    for layout in (UNIFORM, SEGMENTS):
+        r = pkg.Router(n, 4 << 20)
+        try:
+            r.set_alive(alive)
+            r.set_layout(layout)
+            for name, data in _streams(pkg):
+                _assert_same(r.route(data, want_hashes=True), oracle.route(data, n, alive),
+                             f"{name} layout={layout} N={n} dead={dead}")
+                assert r.last_layout() == layout
+        finally:
+            r.close()
+
+
+def test_layouts_full_size_digests(pkg):
+    """The 16 MiB configuration digests (C2..C5) under each forced layout."""
+    for layout in (UNIFORM, SEGMENTS):
+        for key, d in sorted(load_digests().items()):
+            s = pkg.gen_stream(d["nbytes"], d["line_lens"], seed=d["seed"], p_invalid=d["p_invalid"])
+            words = np.array([int(x, 16) for x in d["alive"]], dtype=np.uint64)
+            r = pkg.Router(d["n_downstreams"], d["nbytes"])
+            try:
+                r.set_alive(words)
+                r.set_layout(layout)
+                recs, hs, n = r.route(s.data, want_hashes=True)
+                assert n == d["n_lines"], (key, layout)
+                assert hashlib.sha256(recs.tobytes()).hexdigest() == d["sha256_records"], (key, layout)
+                assert hashlib.sha256(hs.tobytes()).hexdigest() == d["sha256_hashes"], (key, layout)
+            finally:
+                r.close()
+
+
+def test_auto_follows_the_traffic(pkg, oracle):
+    """AUTO: the first launch probes the segment layout; mixed-length traffic keeps it, uniform
+    traffic drops back to the uniform layout until the next probe (every 32nd launch)."""
+    mixed = pkg.gen_stream(4 << 20, [64, 256, 1024], seed=0x5EED0005).data
+    uniform = pkg.gen_stream(4 << 20, [1024], seed=0x5EED0004).data
+    r = pkg.Router(64, 4 << 20)
+    try:
+        seen = []
+        for data in [mixed, mixed, mixed, uniform, uniform, uniform]:
+            _assert_same(r.route(data, want_hashes=True), oracle.route(data, 64), "auto")
+            seen.append(r.last_layout())
+        assert seen[:3] == [SEGMENTS] * 3
+        assert seen[3] == SEGMENTS            # decided before the uniform batch's statistics
+        assert seen[4:] == [UNIFORM, UNIFORM]
+        for _ in range(32 - len(seen)):       # launches 6..31 stay uniform
+            r.route(uniform)
+            assert r.last_layout() == UNIFORM
+        r.route(uniform)                      # launch 32: a probe
+        assert r.last_layout() == SEGMENTS
+    finally:
+        r.close()
+
+
+def test_set_layout_rejects_unknown(pkg):
+    r = pkg.Router(4, 1 << 20)
+    try:
+        with pytest.raises(pkg.SrError):
+            r.set_layout(3)
+        assert r.last_layout() == 0
+    finally:
+        r.close()
