@@ -183,6 +183,38 @@ int sr_pack_many_by_owner(sr_ctx *ctx, const sr_batch *batches, size_t count, ui
                           uint8_t *d_out_bytes, size_t out_cap, sr_record *d_out_recs,
                           uint64_t *d_owner_counts);
 
+/* ---- multi-GPU exchange of owner packs (RCCL over xGMI) -------------------------------------- */
+/* One process per GPU; shard s is owned by GPU s % world. After sr_pack_by_owner /
+ * sr_pack_many_by_owner (n_owners = world), two collective calls per route launch move every
+ * owner's lines to it. RCCL is loaded at sr_comm_open (dlopen of librccl.so.1; a copy already in
+ * the process is shared); without it sr_comm_open returns -ENOSYS.
+ *
+ * sr_comm_id: a fresh communicator id, made by one rank and handed to the others out of band.
+ * sr_comm_open: join the communicator as `rank` of `world` on HIP device `device` (collective:
+ *   every rank calls it). Returns 0, -EINVAL, -ENOSYS (no RCCL), -EIO. */
+#define SR_COMM_ID_BYTES 128u
+typedef struct sr_comm sr_comm;
+int sr_comm_id(uint8_t id[SR_COMM_ID_BYTES]);
+int sr_comm_open(sr_comm **comm, const uint8_t id[SR_COMM_ID_BYTES], int world, int rank, int device);
+void sr_comm_close(sr_comm *comm);
+
+/* Collective, on the context's stream: all-to-all of the split sizes d_owner_counts (u64
+ * [world][2] {lines, bytes} per owner, the pack's output) into d_recv_counts (u64 [world][2] per
+ * source rank), then one copy of both to the host: h_sent / h_received (u64 [world][2]) are valid
+ * on return (the stream is synchronised: the launch's one host round trip). Returns 0, -EINVAL,
+ * -EIO. */
+int sr_exchange_sizes(sr_ctx *ctx, sr_comm *comm, const uint64_t *d_owner_counts, uint64_t *d_recv_counts,
+                      uint64_t *h_sent, uint64_t *h_received);
+
+/* Collective, asynchronous on the context's stream: every owner chunk of d_packed / d_packed_recs
+ * (the pack's output) goes to its owner; the chunks received from sources 0, 1, ... land back to
+ * back in d_recv_bytes (sum of h_received bytes) and d_recv_recs (sum of h_received lines), each
+ * record's offset rebased into d_recv_bytes. Per source, every shard's lines keep their input
+ * order. h_sent / h_received as sr_exchange_sizes returned them. Returns 0, -EINVAL, -EIO. */
+int sr_exchange_data(sr_ctx *ctx, sr_comm *comm, const uint8_t *d_packed, const sr_record *d_packed_recs,
+                     const uint64_t *h_sent, const uint64_t *h_received, uint8_t *d_recv_bytes,
+                     sr_record *d_recv_recs);
+
 /* ---- per-downstream MTU packing ------------------------------------------ */
 /* push_to_downstream (sr-main.c:73-83) appends each routed line to its downstream's active buffer,
  * flushing the buffer first when the line would not fit in DOWNSTREAM_BUF_SIZE (1450) bytes

@@ -50,9 +50,11 @@ ABI_FUNCTIONS = (
     "sr_last_layout",
     "sr_route_batch", "sr_last_probed_dead", "sr_route_device", "sr_route_device_many", "sr_pack_by_owner",
     "sr_pack_many_by_owner", "sr_pack_packets", "sr_pack_packets_many", "sr_route_pack_batch", "sr_alloc_host", "sr_free_host", "sr_sync", "sr_close", "sr_version",
+    "sr_comm_id", "sr_comm_open", "sr_comm_close", "sr_exchange_sizes", "sr_exchange_data",
 )
 SR_MAX_PACK_DOWNSTREAMS = 4096
 SR_LAYOUT_AUTO, SR_LAYOUT_UNIFORM, SR_LAYOUT_SEGMENTS = 0, 1, 2
+SR_COMM_ID_BYTES = 128
 LAYOUT_NAMES = {0: "none", 1: "uniform", 2: "segments"}
 PACKET_DTYPE = np.dtype([("first", "<u4"), ("nlines", "<u2"), ("shard", "<u2"), ("length", "<u2"),
                          ("carry", "<u2"), ("open", "<u4")])
@@ -151,6 +153,11 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_sync": (ctypes.c_int, [vp]),
         "sr_close": (None, [vp]),
         "sr_version": (ctypes.c_char_p, []),
+        "sr_comm_id": (ctypes.c_int, [vp]),
+        "sr_comm_open": (ctypes.c_int, [ctypes.POINTER(vp), vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+        "sr_comm_close": (None, [vp]),
+        "sr_exchange_sizes": (ctypes.c_int, [vp, vp, vp, vp, vp, vp]),
+        "sr_exchange_data": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp]),
     }
     for name in ABI_FUNCTIONS:
         fn = getattr(lib, name)  # raises AttributeError if the export is missing
@@ -395,8 +402,59 @@ class Router:
             arr[i] = SrPackBatch(*[x or None if j not in (2, 7) else x for j, x in enumerate(b)])
         _check(self._lib.sr_pack_packets_many(self._h, arr, len(batches)), "sr_pack_packets_many")
 
+    def exchange_sizes(self, comm: "Comm", d_owner_counts: int, d_recv_counts: int):
+        """sr_exchange_sizes: returns (sent, received) as u64 [world, 2] {lines, bytes} arrays."""
+        sent = np.zeros((comm.world, 2), dtype=np.uint64)
+        received = np.zeros((comm.world, 2), dtype=np.uint64)
+        vp = ctypes.c_void_p
+        _check(self._lib.sr_exchange_sizes(self._h, comm.handle, vp(d_owner_counts), vp(d_recv_counts),
+                                           sent.ctypes.data, received.ctypes.data), "sr_exchange_sizes")
+        return sent, received
+
+    def exchange_data(self, comm: "Comm", d_packed: int, d_packed_recs: int, sent: np.ndarray,
+                      received: np.ndarray, d_recv_bytes: int, d_recv_recs: int) -> None:
+        """sr_exchange_data (asynchronous on the router's stream)."""
+        sent = np.ascontiguousarray(sent, dtype=np.uint64)
+        received = np.ascontiguousarray(received, dtype=np.uint64)
+        vp = ctypes.c_void_p
+        _check(self._lib.sr_exchange_data(self._h, comm.handle, vp(d_packed), vp(d_packed_recs), sent.ctypes.data,
+                                          received.ctypes.data, vp(d_recv_bytes), vp(d_recv_recs)),
+               "sr_exchange_data")
+
     def sync(self) -> None:
         _check(self._lib.sr_sync(self._h), "sr_sync")
+
+
+class Comm:
+    """An RCCL communicator of the C ABI (sr_comm_open): `world` ranks, one GPU each."""
+
+    def __init__(self, comm_id: bytes, world: int, rank: int, device: int):
+        self._lib = lib()
+        if len(comm_id) != SR_COMM_ID_BYTES:
+            raise ValueError("communicator id must be SR_COMM_ID_BYTES bytes")
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(bytes(comm_id), SR_COMM_ID_BYTES)
+        _check(self._lib.sr_comm_open(ctypes.byref(h), buf, world, rank, device), "sr_comm_open")
+        self.handle, self.world, self.rank, self.device = h, world, rank, device
+
+    @staticmethod
+    def new_id() -> bytes:
+        buf = ctypes.create_string_buffer(SR_COMM_ID_BYTES)
+        _check(lib().sr_comm_id(buf), "sr_comm_id")
+        return buf.raw
+
+    @classmethod
+    def from_group(cls, device: int, group=None) -> "Comm":
+        """Every rank of a torch.distributed group joins one communicator (rank 0 makes the id)."""
+        import torch.distributed as dist
+        box = [cls.new_id() if dist.get_rank(group) == 0 else None]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        return cls(box[0], dist.get_world_size(group), dist.get_rank(group), device)
+
+    def close(self) -> None:
+        if self.handle:
+            self._lib.sr_comm_close(self.handle)
+            self.handle = ctypes.c_void_p()
 
 
 def version() -> str:

@@ -1441,6 +1441,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     wg_barrier();
                 }
             }
+            if (wbase == 0) stamp<ABL>(p, tid, g, 14);   // after the segment pre-pass
             if ((ABL & KV_SEGMENTS) && last_win && tid == 0) {   // the layout statistics (arrive)
                 __hip_atomic_fetch_add(&p.ctl->layout[g & 7u][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (gain2)

@@ -15,6 +15,7 @@
 #include <new>
 
 #include "../../include/sr_route.h"
+#include "exchange.hpp"
 #include "mtu_kernel.hpp"
 #include "regroup_kernel.hpp"
 #include "route_host.hpp"
@@ -536,6 +537,123 @@ int sr_route_batch(sr_ctx *c, const uint8_t *bytes, size_t nbytes, sr_record *ou
     }
     *n_records = (size_t)n;
     return n > max_records ? -ENOSPC : 0;
+}
+
+}  // extern "C"
+
+// ---- multi-GPU exchange (exchange.hpp) ----------------------------------------------------------
+struct sr_comm {
+    void *nccl;
+    int world, rank, device;
+    uint64_t *h_sizes;   // pinned: [2][world][2] sent, received
+};
+
+extern "C" {
+
+int sr_comm_id(uint8_t id[SR_COMM_ID_BYTES]) {
+    RcclApi *r = rccl_api();
+    if (!id) return -EINVAL;
+    if (!r) return -ENOSYS;
+    return r->get_unique_id(id) == 0 ? 0 : -EIO;
+}
+
+int sr_comm_open(sr_comm **out, const uint8_t id[SR_COMM_ID_BYTES], int world, int rank, int device) {
+    if (!out || !id || world < 1 || world > (int)kMaxOwners || rank < 0 || rank >= world) return -EINVAL;
+    *out = nullptr;
+    RcclApi *r = rccl_api();
+    if (!r) return -ENOSYS;
+    if (hipSetDevice(device) != hipSuccess) return -ENODEV;
+    sr_comm *c = new (std::nothrow) sr_comm{nullptr, world, rank, device, nullptr};
+    if (!c) return -ENOMEM;
+    if (hipHostMalloc((void **)&c->h_sizes, 4 * (size_t)world * sizeof(uint64_t)) != hipSuccess) {
+        delete c;
+        return -ENOMEM;
+    }
+    CommId cid;
+    memcpy(cid.b, id, sizeof(cid.b));
+    if (((InitRankFn)r->comm_init_rank)(&c->nccl, world, cid, rank) != 0) {
+        (void)hipHostFree(c->h_sizes);
+        delete c;
+        return -EIO;
+    }
+    *out = c;
+    return 0;
+}
+
+void sr_comm_close(sr_comm *c) {
+    if (!c) return;
+    RcclApi *r = rccl_api();
+    if (r && c->nccl) (void)r->comm_destroy(c->nccl);
+    (void)hipHostFree(c->h_sizes);
+    delete c;
+}
+
+int sr_exchange_sizes(sr_ctx *ctx, sr_comm *comm, const uint64_t *d_owner_counts, uint64_t *d_recv_counts,
+                      uint64_t *h_sent, uint64_t *h_received) {
+    if (!ctx || !comm || !d_owner_counts || !d_recv_counts || !h_sent || !h_received) return -EINVAL;
+    RcclApi *r = rccl_api();
+    if (!r) return -ENOSYS;
+    (void)hipSetDevice(ctx->device);
+    const size_t w2 = 2 * (size_t)comm->world;
+    if (r->all_to_all(d_owner_counts, d_recv_counts, 2, kNcclUint64, comm->nccl, ctx->stream) != 0) return -EIO;
+    if (hipMemcpyAsync(comm->h_sizes, d_owner_counts, w2 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream) !=
+            hipSuccess ||
+        hipMemcpyAsync(comm->h_sizes + w2, d_recv_counts, w2 * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                       ctx->stream) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess)
+        return -EIO;
+    memcpy(h_sent, comm->h_sizes, w2 * sizeof(uint64_t));
+    memcpy(h_received, comm->h_sizes + w2, w2 * sizeof(uint64_t));
+    return 0;
+}
+
+int sr_exchange_data(sr_ctx *ctx, sr_comm *comm, const uint8_t *d_packed, const sr_record *d_packed_recs,
+                     const uint64_t *h_sent, const uint64_t *h_received, uint8_t *d_recv_bytes,
+                     sr_record *d_recv_recs) {
+    if (!ctx || !comm || !h_sent || !h_received) return -EINVAL;
+    RcclApi *r = rccl_api();
+    if (!r) return -ENOSYS;
+    const int G = comm->world;
+    uint64_t s_l = 0, s_b = 0, r_l = 0, r_b = 0;
+    RebaseArgs a;
+    memset(&a, 0, sizeof(a));
+    for (int q = 0; q < G; ++q) {
+        a.line0[q] = (uint32_t)r_l;
+        a.byte0[q] = (uint32_t)r_b;
+        s_l += h_sent[2 * q];
+        s_b += h_sent[2 * q + 1];
+        r_l += h_received[2 * q];
+        r_b += h_received[2 * q + 1];
+    }
+    if (r_b > 0xFFFFFFFFull || r_l > 0xFFFFFFFFull) return -EINVAL;   // record offsets are u32
+    if ((s_b && !d_packed) || (s_l && !d_packed_recs) || (r_b && !d_recv_bytes) || (r_l && !d_recv_recs))
+        return -EINVAL;
+    a.sources = (uint32_t)G;
+    a.n_lines = (uint32_t)r_l;
+    a.line0[G] = (uint32_t)r_l;
+    (void)hipSetDevice(ctx->device);
+    if (r->group_start() != 0) return -EIO;
+    int bad = 0;
+    uint64_t so_l = 0, so_b = 0, ro_l = 0, ro_b = 0;
+    for (int q = 0; q < G; ++q) {
+        const uint64_t sl = h_sent[2 * q], sb = h_sent[2 * q + 1];
+        const uint64_t rl = h_received[2 * q], rb = h_received[2 * q + 1];
+        if (sb) bad |= r->send(d_packed + so_b, sb, kNcclUint8, q, comm->nccl, ctx->stream);
+        if (rb) bad |= r->recv(d_recv_bytes + ro_b, rb, kNcclUint8, q, comm->nccl, ctx->stream);
+        if (sl) bad |= r->send(d_packed_recs + so_l, sl, kNcclUint64, q, comm->nccl, ctx->stream);
+        if (rl) bad |= r->recv(d_recv_recs + ro_l, rl, kNcclUint64, q, comm->nccl, ctx->stream);
+        so_l += sl;
+        so_b += sb;
+        ro_l += rl;
+        ro_b += rb;
+    }
+    if (r->group_end() != 0 || bad) return -EIO;
+    if (r_l) {
+        hipLaunchKernelGGL(exchange_rebase_kernel, dim3((uint32_t)((r_l + 255) / 256)), dim3(256), 0, ctx->stream,
+                           d_recv_recs, a);
+        if (hipGetLastError() != hipSuccess) return -EIO;
+    }
+    return 0;
 }
 
 }  // extern "C"

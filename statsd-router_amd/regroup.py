@@ -13,6 +13,7 @@ pushes them.
 """
 from __future__ import annotations
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -152,8 +153,10 @@ class LaunchRegrouper:
     all-to-all of the split sizes with one host round trip, then the packed lines and the records
     (RCCL over xGMI with the "nccl" backend; gloo in the CPU tests). Same stream rule as Regrouper."""
 
-    def __init__(self, pkg, router, max_total_bytes: int, max_total_records: int, group=None):
-        self.pkg, self.router, self.group = pkg, router, group
+    def __init__(self, pkg, router, max_total_bytes: int, max_total_records: int, group=None, comm=None):
+        """comm: a pkg.Comm for the C-ABI exchange (sr_exchange_sizes / sr_exchange_data over RCCL);
+        None: torch.distributed collectives on `group` (gloo in the CPU tests, nccl on GPUs)."""
+        self.pkg, self.router, self.group, self.comm = pkg, router, group, comm
         self.G = dist.get_world_size(group)
         if not 1 <= self.G <= pkg.SR_MAX_OWNERS:
             raise ValueError(f"regroup over {self.G} ranks: at most {pkg.SR_MAX_OWNERS}")
@@ -177,5 +180,16 @@ class LaunchRegrouper:
             raise ValueError("launch larger than the regrouper's buffers")
         self.router.pack_many_by_owner(batches, self.G, self.bytes.data_ptr(), self.cap, self.recs.data_ptr(),
                                        self.counts.data_ptr())
-        rb, rr, rc, self.last_sent, self.last_received = _exchange(self.bytes, self.recs, self.counts, self.group)
-        return rb, rr, rc
+        if self.comm is None:
+            rb, rr, rc, self.last_sent, self.last_received = _exchange(self.bytes, self.recs, self.counts, self.group)
+            return rb, rr, rc
+        # the C ABI: one size exchange (one host round trip), then the grouped sends and the rebase
+        rc = torch.empty((self.G, 2), dtype=torch.int64, device=self.bytes.device)
+        sent, received = self.router.exchange_sizes(self.comm, self.counts.data_ptr(), rc.data_ptr())
+        n_l, n_b = int(received[:, 0].sum()), int(received[:, 1].sum())
+        rb = torch.empty(max(n_b, 1), dtype=torch.uint8, device=self.bytes.device)
+        rr = torch.empty(max(n_l, 1), dtype=torch.int64, device=self.bytes.device)
+        self.router.exchange_data(self.comm, self.bytes.data_ptr(), self.recs.data_ptr(), sent, received,
+                                  rb.data_ptr(), rr.data_ptr())
+        self.last_sent, self.last_received = sent.astype(np.int64).tolist(), received.astype(np.int64).tolist()
+        return rb[:n_b], rr[:n_l], rc

@@ -142,3 +142,91 @@ def test_pack_many_by_owner_matches_oracle(pkg, oracle, G, n_shards, nb, torch_s
     assert np.array_equal(d_pb[: eb.size].cpu().numpy(), eb)
     got = np.frombuffer(d_pr[: len(er)].cpu().numpy().tobytes(), dtype=pkg.RECORD_DTYPE)
     assert np.array_equal(got, er)
+
+
+def test_c_exchange_one_rank(pkg, oracle, torch_stream):
+    """The C-ABI exchange (sr_comm_* / sr_exchange_sizes / sr_exchange_data over RCCL) on a one-rank
+    communicator, without torch.distributed: the launch's packs come back rebased, equal to the
+    oracle's pack."""
+    import torch
+
+    streams = [pkg.gen_stream(1 << 19, [64, 256, 1024], seed=700 + b, p_invalid=0.05) for b in range(3)]
+    cap = max(s.n_lines for s in streams)
+    d_in = torch.zeros((3, 1 << 19), dtype=torch.uint8, device="cuda")
+    for b, s in enumerate(streams):
+        d_in[b, : s.data.size].copy_(torch.from_numpy(s.data))
+    d_rec = torch.zeros((3, cap), dtype=torch.int64, device="cuda")
+    d_n = torch.zeros(3, dtype=torch.int64, device="cuda")
+    total = sum(int(s.data.size) for s in streams)
+    out_cap = pkg.pack_capacity(total)
+    d_pb = torch.zeros(out_cap, dtype=torch.uint8, device="cuda")
+    d_pr = torch.zeros(3 * cap, dtype=torch.int64, device="cuda")
+    d_cnt = torch.zeros((1, 2), dtype=torch.int64, device="cuda")
+    d_rc = torch.zeros((1, 2), dtype=torch.int64, device="cuda")
+    comm = pkg.Comm(pkg.Comm.new_id(), 1, 0, 0)
+    try:
+        with pkg.Router(32, 1 << 19) as r:
+            r.set_stream(torch_stream.cuda_stream)
+            batches = [(d_in[b].data_ptr(), int(s.data.size), d_rec[b].data_ptr(), cap, d_n[b].data_ptr())
+                       for b, s in enumerate(streams)]
+            r.route_device_many([(db, nb, dr, mr, None, dn) for db, nb, dr, mr, dn in batches])
+            r.pack_many_by_owner(batches, 1, d_pb.data_ptr(), out_cap, d_pr.data_ptr(), d_cnt.data_ptr())
+            sent, received = r.exchange_sizes(comm, d_cnt.data_ptr(), d_rc.data_ptr())
+            assert sent.tolist() == received.tolist()
+            n_l, n_b = int(received[:, 0].sum()), int(received[:, 1].sum())
+            rb = torch.full((n_b + 64,), 0xCD, dtype=torch.uint8, device="cuda")
+            rr = torch.zeros(n_l, dtype=torch.int64, device="cuda")
+            r.exchange_data(comm, d_pb.data_ptr(), d_pr.data_ptr(), sent, received, rb.data_ptr(), rr.data_ptr())
+            r.sync()
+    finally:
+        comm.close()
+    recs_list = [oracle.route(s.data, 32)[0] for s in streams]
+    eb, er, ec = oracle.pack_many_by_owner([s.data for s in streams], recs_list, 1)
+    assert received.astype(np.int64).tolist() == ec.tolist() == d_rc.cpu().numpy().tolist()
+    got_b = rb.cpu().numpy()
+    assert np.array_equal(got_b[:n_b], eb) and (got_b[n_b:] == 0xCD).all()
+    assert np.array_equal(rr.cpu().numpy().view(pkg.RECORD_DTYPE), er)
+
+
+def test_launch_regrouper_c_exchange(pkg, oracle, torch_stream):
+    """LaunchRegrouper with a pkg.Comm made from the torch.distributed group (one rank here): the
+    same result as the torch.distributed exchange."""
+    import torch
+    import torch.distributed as dist
+
+    rg = importlib.import_module("statsd-router_amd.regroup")
+    store = dist.TCPStore("127.0.0.1", 0, 1, True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1)
+    comm = None
+    try:
+        comm = pkg.Comm.from_group(0)
+        streams = [pkg.gen_stream(1 << 19, [64, 1024], seed=800 + b, p_invalid=0.1) for b in range(4)]
+        cap = max(s.n_lines for s in streams)
+        d_in = torch.zeros((4, 1 << 19), dtype=torch.uint8, device="cuda")
+        for b, s in enumerate(streams):
+            d_in[b, : s.data.size].copy_(torch.from_numpy(s.data))
+        d_rec = torch.zeros((4, cap), dtype=torch.int64, device="cuda")
+        d_n = torch.zeros(4, dtype=torch.int64, device="cuda")
+        total = sum(int(s.data.size) for s in streams)
+        with pkg.Router(16, 1 << 19) as r:
+            r.set_stream(torch_stream.cuda_stream)
+            batches = [(d_in[b].data_ptr(), int(s.data.size), d_rec[b].data_ptr(), cap, d_n[b].data_ptr())
+                       for b, s in enumerate(streams)]
+            r.route_device_many([(db, nb, dr, mr, None, dn) for db, nb, dr, mr, dn in batches])
+            out = {}
+            for name, c in (("torch", None), ("c", comm)):
+                reg = rg.LaunchRegrouper(pkg, r, total, 4 * cap, comm=c)
+                rb, rr, rc = reg(batches)
+                torch.cuda.synchronize()
+                out[name] = (rb.cpu().numpy(), rr.cpu().numpy(), rc.cpu().numpy().tolist(), reg.last_received)
+        assert np.array_equal(out["torch"][0], out["c"][0])
+        assert np.array_equal(out["torch"][1], out["c"][1])
+        assert out["torch"][2] == out["c"][2] and out["torch"][3] == out["c"][3]
+        recs_list = [oracle.route(s.data, 16)[0] for s in streams]
+        eb, er, ec = oracle.pack_many_by_owner([s.data for s in streams], recs_list, 1)
+        assert np.array_equal(out["c"][0], eb)
+        assert np.array_equal(out["c"][1].view(pkg.RECORD_DTYPE), er)
+    finally:
+        if comm is not None:
+            comm.close()
+        dist.destroy_process_group()

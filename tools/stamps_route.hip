@@ -32,6 +32,8 @@ static double med(std::vector<double> v) {
 
 // one launch over all L batches (the product's multi-batch mode): per-phase medians over every
 // workgroup of the launch, plus the launch span
+static bool seg_layout = false;
+
 template <int BLOCK>
 void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size_t> &sizes, sr_record *d_out,
               size_t max_lines, uint64_t *d_n, uint64_t *d_dbg, hipStream_t s, uint32_t line_len) {
@@ -45,7 +47,8 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
         for (int i = 0; i < L; ++i)
             DeviceState::add_batch(p, batches[i], sizes[i], d_out + (size_t)i * max_lines, max_lines, nullptr, d_n + i);
         p.dbg = d_dbg;
-        launch_route<BLOCK, ABL_STAMPS>(ds, p, s);
+        if (seg_layout) launch_route<BLOCK, ABL_STAMPS | KV_SEGMENTS>(ds, p, s);
+        else launch_route<BLOCK, ABL_STAMPS>(ds, p, s);
     };
     for (int w = 0; w < 3; ++w) launch();
     CK(hipStreamSynchronize(s));
@@ -116,7 +119,7 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
             printf("{\"scanner_poll_rt_us\": [%.2f, %.2f, %.2f, %.2f], \"rounds_per_batch\": %.1f}\n", rt[rt.size() / 10],
                    rt[rt.size() / 2], rt[rt.size() * 9 / 10], rt[rt.size() * 99 / 100], nr / 16.0);
     }
-    std::vector<double> ph[8];
+    std::vector<double> ph[8], ph3b;
     uint64_t s0 = ~0ull, e1 = 0;
     {   // residency: tiles alive over the launch (start stamp 0 .. end stamp 6), in 1 us bins
         std::vector<std::pair<uint64_t, uint64_t>> iv;
@@ -149,6 +152,7 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
         if (d[3]) ph[2].push_back((d[7] - d[3]) * u);   // base wait (tid 0, first record), when polled
         ph[3].push_back((d[4] - d[2]) * u);
         ph[4].push_back((d[5] - d[4]) * u);
+        if (d[14]) ph3b.push_back((d[14] - d[4]) * u);   // segment pre-pass
         ph[5].push_back((d[6] - d[0]) * u);
         ph[6].push_back((d[0] - d[8]) * u);   // entry: epoch, batch lookup, load issue
         ph[7].push_back((d[9] - d[8]) * u);   // entry .. after arrive
@@ -162,24 +166,30 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
     }
     printf("{\"mode\": \"%d batches per launch\", \"block\": %d, \"line_len\": %u, \"tiles\": %u, \"span_us\": %.2f, "
            "\"median_us\": {\"load\": %.2f, \"masks_scan\": %.2f, \"base_wait\": %.2f, \"to_staged\": %.2f, "
-           "\"hash_records\": %.2f, \"lifetime\": %.2f, \"entry\": %.2f, \"entry_to_exit\": %.2f}}\n",
+           "\"hash_records\": %.2f, \"of_which_prepass\": %.2f, \"lifetime\": %.2f, \"entry\": %.2f, \"entry_to_exit\": %.2f}}\n",
            L, BLOCK, line_len, total, (e1 - s0) * 0.01, med(ph[0]), med(ph[1]), med(ph[2]), med(ph[3]), med(ph[4]),
-           med(ph[5]), med(ph[6]), med(ph[7]));
+           med(ph3b), med(ph[5]), med(ph[6]), med(ph[7]));
 }
 
 int main(int argc, char **argv) {
     const int L = 16;
     const size_t batch = 16u << 20;
+    // argv: line length (0 = the C5 mix 64/256/1024), shards, "seg" for the segment layout
     uint32_t line_len = argc > 1 ? (uint32_t)atoi(argv[1]) : 64;
+    const uint32_t nds = argc > 2 ? (uint32_t)atoi(argv[2]) : 4;
+    seg_layout = argc > 3 && !strcmp(argv[3], "seg");
+    uint32_t mix[3] = {64, 256, 1024};
+    const uint32_t *lens = line_len ? &line_len : mix;
+    const uint32_t nlens = line_len ? 1u : 3u;
     CK(hipSetDevice(0));
     DeviceState ds;
-    if (ds.init(batch, 4) != 0) return 1;
+    if (ds.init(batch, nds) != 0) return 1;
     std::vector<uint8_t> host(batch);
     std::vector<uint8_t *> batches;
     std::vector<size_t> sizes;
     size_t nl = 0, nd = 0;
     for (int b = 0; b < L; ++b) {
-        const size_t n = sr_gen_stream(0x5EED0002ull + 65537ull * b, 0, &line_len, 1, 0.0, 4095, host.data(), batch,
+        const size_t n = sr_gen_stream(0x5EED0002ull + 65537ull * b, 0, lens, nlens, 0.0, 4095, host.data(), batch,
                                        nullptr, 0, &nd, &nl);
         uint8_t *d;
         CK(hipMalloc(&d, batch));
