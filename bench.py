@@ -71,6 +71,9 @@ def parse(argv=None):
                     help="classify + all-to-all regroup leg (auto: on when more than one GPU)")
     ap.add_argument("--regroup-config", default="c5", choices=sorted(CONFIGS))
     ap.add_argument("--regroup-steps", type=int, default=8)
+    ap.add_argument("--regroup-batches", type=int, default=32, help="batches per regroup step (one route launch)")
+    ap.add_argument("--exchange", default="c", choices=["c", "torch"],
+                    help="regroup transport: the C ABI's RCCL exchange or torch.distributed")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -316,7 +319,8 @@ def main(argv=None):
     del d_in, d_out
     torch.cuda.empty_cache()
     if args.regroup == "on" or (args.regroup == "auto" and world > 1):
-        rg = regroup_leg(pkg, dev, local, world, rank, args.regroup_config, args.regroup_steps)
+        rg = regroup_leg(pkg, dev, local, world, rank, args.regroup_config, args.regroup_steps,
+                         per_step=args.regroup_batches, exchange=args.exchange)
         if rank == 0:
             result["regroup"] = rg
     if rank == 0:
@@ -430,7 +434,7 @@ def cpu_baseline(host, shards, alive, seconds):
     }, **common)
 
 
-def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8):
+def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8, exchange="c"):
     """Classify + regroup on its own batches of config `cfg` (C5 by default: mixed
     lengths, 64 shards). One step = one route launch of `per_step` batches, then ONE pack of all of
     them by owner GPU (shard % G, sr_pack_many_by_owner) and ONE exchange: an all-to-all of the
@@ -463,8 +467,15 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8):
     pack_descs = [(base + b * batch_bytes, sizes[b], d_rec[b].data_ptr(), max_lines, d_n[b].data_ptr())
                   for b in range(nb)]
 
+    comm, transport = None, "torch.distributed all_to_all_single (nccl)"
+    if exchange == "c":   # the C ABI's RCCL exchange (sr_exchange_sizes / sr_exchange_data)
+        try:
+            comm = pkg.Comm.from_group(local)
+            transport = "C ABI sr_exchange_sizes + sr_exchange_data (RCCL)"
+        except (OSError, RuntimeError) as e:
+            transport += f" (sr_comm_open failed: {e})"
     with torch.cuda.stream(stream):
-        reg = rg_mod.LaunchRegrouper(pkg, router, sum(sizes), nb * max_lines)
+        reg = rg_mod.LaunchRegrouper(pkg, router, sum(sizes), nb * max_lines, comm=comm)
 
         def step():
             router.route_device_many(route_descs)
@@ -484,6 +495,8 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8):
         dist.barrier()
         wall = time.perf_counter() - t0
     router.close()
+    if comm is not None:
+        comm.close()
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
     tot = torch.tensor([sum(lines) * steps, acc[0], acc[1], acc[2]], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -492,7 +505,7 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8):
     return {"value": round(float(tot[0]) / w / 1e6, 3), "unit": "M metrics/s", "workload": desc,
             "steps_per_gpu": steps, "batches_per_step": nb, "ms_per_step": round(w * 1e3 / steps, 4),
             "lines_regrouped": int(tot[1]), "bytes_regrouped": int(tot[2]),
-            "bytes_sent_to_other_gpus_per_s": round(float(tot[3]) / w / 1e9, 3),
+            "bytes_sent_to_other_gpus_per_s": round(float(tot[3]) / w / 1e9, 3), "exchange": transport,
             "note": (f"route launch of {nb} x 16 MiB batches + one sr_pack_many_by_owner + one exchange (split sizes, "
                      f"packed lines, records) per step over {world} GPU(s); owner = shard % {world}; one host round "
                      f"trip per step for the split sizes")}

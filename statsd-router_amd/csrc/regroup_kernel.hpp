@@ -22,7 +22,8 @@
 namespace srk {
 
 constexpr int kPackBlock = 256;
-constexpr int kPackChunks = 8;                          // 256-record chunks per tile
+constexpr int kPackChunks = 2;                          // 256-record chunks per tile (long lines:
+                                                        // enough tiles to fill the chip)
 constexpr int kPackTile = kPackBlock * kPackChunks;     // records per tile
 constexpr int kMaxOwners = 64;
 
@@ -224,18 +225,50 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
         }
         // copy the chunk's lines: 16 lanes per line, one dword per lane per pass, 4-byte aligned
         // destination, source realigned from two aligned dwords (buffer loads: no fault past the end)
+        // 16 lanes per line, 16 bytes per lane per pass: one dwordx4 and one dword load (the
+        // source realigned by v_alignbyte), a dwordx4 store where the padded line covers all of it;
+        // the loads of kCopyBatch passes are issued before their stores
+        constexpr int kCopyBatch = 4;
         const int sub = tid & 15;
         for (int k = tid >> 4; k < kPackBlock; k += kPackBlock / 16) {
             const uint32_t L = s_len[k];
             if (L == 0) continue;
             const uint32_t src = s_src[k], d = s_dst[k];
             const uint32_t sh = src & 3u, sa = src & ~3u;
-            for (uint32_t q = 4u * sub; q < L; q += 64u) {
-                const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(rsrc, sa + q, 0, 0);
-                const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(rsrc, sa + q + 4u, 0, 0);
-                uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, sh);
-                if (q + 4u > L) v &= (1u << (8u * (L - q))) - 1u;   // zero fill after the line
-                if ((uint64_t)d + q + 4u <= p.out_cap) *(uint32_t *)(p.out_bytes + d + q) = v;
+            const uint32_t L4 = pack_len4(L);
+            for (uint32_t q0 = 16u * sub; q0 < L; q0 += 256u * kCopyBatch) {
+                uint4 v[kCopyBatch];
+#pragma unroll
+                for (int i = 0; i < kCopyBatch; ++i) {
+                    const uint32_t q = q0 + 256u * i;
+                    v[i] = make_uint4(0, 0, 0, 0);
+                    if (q < L) {
+                        const v4u32 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, sa + q, 0, 0);
+                        const uint32_t e = __builtin_amdgcn_raw_buffer_load_b32(rsrc, sa + q + 16u, 0, 0);
+                        v[i] = make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], sh), __builtin_amdgcn_alignbyte(x[2], x[1], sh),
+                                          __builtin_amdgcn_alignbyte(x[3], x[2], sh), __builtin_amdgcn_alignbyte(e, x[3], sh));
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < kCopyBatch; ++i) {
+                    const uint32_t q = q0 + 256u * i;
+                    if (q >= L) break;
+                    uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {   // zero fill after the line
+                        const uint32_t qj = q + 4u * j;
+                        if (qj >= L) w[j] = 0;
+                        else if (qj + 4u > L) w[j] &= (1u << (8u * (L - qj))) - 1u;
+                    }
+                    uint8_t *o = p.out_bytes + d + q;
+                    if (q + 16u <= L4 && (uint64_t)d + q + 16u <= p.out_cap) {
+                        *(uint4 *)o = make_uint4(w[0], w[1], w[2], w[3]);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            if (q + 4u * j < L4 && (uint64_t)d + q + 4u * j + 4u <= p.out_cap) ((uint32_t *)o)[j] = w[j];
+                    }
+                }
             }
         }
         __syncthreads();

@@ -635,19 +635,31 @@ int sr_exchange_data(sr_ctx *ctx, sr_comm *comm, const uint8_t *d_packed, const 
     if (r->group_start() != 0) return -EIO;
     int bad = 0;
     uint64_t so_l = 0, so_b = 0, ro_l = 0, ro_b = 0;
+    uint64_t self_so_l = 0, self_so_b = 0, self_ro_l = 0, self_ro_b = 0;
     for (int q = 0; q < G; ++q) {
         const uint64_t sl = h_sent[2 * q], sb = h_sent[2 * q + 1];
         const uint64_t rl = h_received[2 * q], rb = h_received[2 * q + 1];
-        if (sb) bad |= r->send(d_packed + so_b, sb, kNcclUint8, q, comm->nccl, ctx->stream);
-        if (rb) bad |= r->recv(d_recv_bytes + ro_b, rb, kNcclUint8, q, comm->nccl, ctx->stream);
-        if (sl) bad |= r->send(d_packed_recs + so_l, sl, kNcclUint64, q, comm->nccl, ctx->stream);
-        if (rl) bad |= r->recv(d_recv_recs + ro_l, rl, kNcclUint64, q, comm->nccl, ctx->stream);
+        if (q == comm->rank) {   // our own chunk: a device copy below, not a send to ourselves
+            self_so_l = so_l, self_so_b = so_b, self_ro_l = ro_l, self_ro_b = ro_b;
+        } else {
+            if (sb) bad |= r->send(d_packed + so_b, sb, kNcclUint8, q, comm->nccl, ctx->stream);
+            if (rb) bad |= r->recv(d_recv_bytes + ro_b, rb, kNcclUint8, q, comm->nccl, ctx->stream);
+            if (sl) bad |= r->send(d_packed_recs + so_l, sl, kNcclUint64, q, comm->nccl, ctx->stream);
+            if (rl) bad |= r->recv(d_recv_recs + ro_l, rl, kNcclUint64, q, comm->nccl, ctx->stream);
+        }
         so_l += sl;
         so_b += sb;
         ro_l += rl;
         ro_b += rb;
     }
     if (r->group_end() != 0 || bad) return -EIO;
+    const uint64_t own_l = h_sent[2 * comm->rank], own_b = h_sent[2 * comm->rank + 1];
+    if (own_l != h_received[2 * comm->rank] || own_b != h_received[2 * comm->rank + 1]) return -EINVAL;
+    if ((own_b && hipMemcpyAsync(d_recv_bytes + self_ro_b, d_packed + self_so_b, own_b, hipMemcpyDeviceToDevice,
+                                 ctx->stream) != hipSuccess) ||
+        (own_l && hipMemcpyAsync(d_recv_recs + self_ro_l, d_packed_recs + self_so_l, own_l * sizeof(sr_record),
+                                 hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess))
+        return -EIO;
     if (r_l) {
         hipLaunchKernelGGL(exchange_rebase_kernel, dim3((uint32_t)((r_l + 255) / 256)), dim3(256), 0, ctx->stream,
                            d_recv_recs, a);
