@@ -239,6 +239,7 @@ def main(argv=None):
     verify = None if args.no_verify else verify_timed_launch(pkg, graphs[0], stream, d_out, host, M, max_lines,
                                                              shards, alive, rank, digests, dkey, alive_tag)
 
+    ceiling = read_ceiling(d_in, stream)
     wall = t1 - t0
     steps_lines = sum(group_lines[i % ng] for i in range(K))
     steps_bytes = sum(group_bytes[i % ng] for i in range(K))
@@ -300,6 +301,8 @@ def main(argv=None):
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "kernel": "route_kernel",
+                "read_ceiling": dict(ceiling, frac_of_ceiling=round(achieved / ceiling["achieved"], 4))
+                if ceiling.get("achieved") else ceiling,
                 "bytes_per_launch": steps_bytes / K,
                 "launch_us": round(region_ms * 1e3 / K, 3),
                 "launch_timing": (f"timed region: {K} back-to-back launches between two HIP events on the launch "
@@ -327,6 +330,36 @@ def main(argv=None):
         print(json.dumps(result), file=json_out, flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+
+
+def read_ceiling(d_in, stream, reps=20):
+    """SURVEY.md §8d's measured streaming-read ceiling: a read-only kernel (tools/hbm/hbm_read.hip,
+    16 B per lane, 8 loads in flight) over the same resident batches, timed with HIP events on the
+    launch stream. Returns {"achieved": GB/s, ...} or a note when the tool library is absent."""
+    import ctypes
+    import torch
+
+    path = os.path.join(REPO, "tools", "hbm", "libsr_hbm.so")
+    if not os.path.exists(path):
+        return {"note": f"{path} not built"}
+    lib = ctypes.CDLL(path)
+    lib.sr_hbm_read.restype = ctypes.c_int
+    lib.sr_hbm_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]
+    n = d_in.numel() & ~15
+    blocks = 4096
+    out = torch.empty(blocks, dtype=torch.int32, device=d_in.device)
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            lib.sr_hbm_read(d_in.data_ptr(), n, out.data_ptr(), blocks, stream.cuda_stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            lib.sr_hbm_read(d_in.data_ptr(), n, out.data_ptr(), blocks, stream.cuda_stream)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return {"achieved": round(n / (ms * 1e-3) / 1e9, 1), "unit": "GB/s", "bytes": int(n),
+            "kernel": "tools/hbm/hbm_read.hip: read-only, nontemporal 16-B loads, 4096 x 256 threads"}
 
 
 def verify_timed_launch(pkg, graph, stream, d_out, host, M, max_lines, shards, alive, rank, digests, dkey, tag):
