@@ -1376,7 +1376,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 if (act && gi == 0) finish(j, s, len, len_ok, fmt_ok, h);
             };
             // Lanes per line. A tile whose longest name fits its G lanes in one pass (uniform
-            // lengths: C2, C4) keeps one G-lane group per line (G = 1: no pre-pass at all). A tile
+            // lengths: C2, C4) keeps one G-lane group per line (the KV_UNIFORM kernel always). A tile
             // of mixed lengths (C5: a 64-byte line next to 1024-byte ones) gets one lane per
             // 64-byte name segment instead, the lines packed back to back over the lanes: no idle
             // lanes, one segment per lane.
@@ -1386,7 +1386,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
             // (the segment variant decides in a tile's last window, after which the lane masks and
             // line states of later windows are dead)
             const bool last_win = wbase + kWin >= (int)tile_count;
-            if ((ABL & KV_SEGMENTS) && last_win && G > 1) {
+            if ((ABL & KV_SEGMENTS) && last_win) {
                 // per line: 64-byte name segments, and lane units of one or two segments (two
                 // when one-segment units would take a second round of lanes)
                 uint32_t want = 0, nsg = 0;

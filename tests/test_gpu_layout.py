@@ -25,6 +25,8 @@ def _streams(pkg):
     yield "lengths_1_to_1600", _lines_stream(rng.integers(1, 1600, 3000).tolist(), seed=9)
     yield "short_and_1449", _lines_stream([6, 1449, 7, 64, 1449, 1449, 9, 200] * 400, seed=10)
     yield "empty_names", b"".join([b":1|c\n", b"x" * 900 + b":v\n", b"ab:\n", b":\n"] * 500)
+    # mean under 64 B (G = 1) with long lines among the short: two-segment units over two rounds
+    yield "tiny_and_1449_two_rounds", _lines_stream(([6] * 15 + [1449]) * 300, seed=11)
     yield "dense_newlines", b"\n" * 40_000 + _lines_stream([6] * 9000, seed=3) + b"\n" * 100
     yield "hostile", pkg.frame_datagrams(_hostile_stream(7, 300_000))
 
