@@ -322,8 +322,11 @@ def main(argv=None):
     del d_in, d_out
     torch.cuda.empty_cache()
     if args.regroup == "on" or (args.regroup == "auto" and world > 1):
-        rg = regroup_leg(pkg, dev, local, world, rank, args.regroup_config, args.regroup_steps,
-                         per_step=args.regroup_batches, exchange=args.exchange)
+        try:   # a failing regroup leg must not take the main line with it
+            rg = regroup_leg(pkg, dev, local, world, rank, args.regroup_config, args.regroup_steps,
+                             per_step=args.regroup_batches, exchange=args.exchange)
+        except (RuntimeError, OSError, ValueError) as e:
+            rg = {"error": f"{type(e).__name__}: {e}"}
         if rank == 0:
             result["regroup"] = rg
     if rank == 0:
