@@ -505,11 +505,20 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8, exchange="
 
     comm, transport = None, "torch.distributed all_to_all_single (nccl)"
     if exchange == "c":   # the C ABI's RCCL exchange (sr_exchange_sizes / sr_exchange_data)
+        err = ""
         try:
             comm = pkg.Comm.from_group(local)
-            transport = "C ABI sr_exchange_sizes + sr_exchange_data (RCCL)"
         except (OSError, RuntimeError) as e:
-            transport += f" (sr_comm_open failed: {e})"
+            err = str(e)
+        ok = torch.tensor([0.0 if comm is None else 1.0], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)   # every rank on the same transport
+        if ok.item() == 1.0:
+            transport = "C ABI sr_exchange_sizes + sr_exchange_data (RCCL)"
+        else:
+            if comm is not None:
+                comm.close()
+                comm = None
+            transport += f" (sr_comm_open failed on some rank{': ' + err if err else ''})"
     with torch.cuda.stream(stream):
         reg = rg_mod.LaunchRegrouper(pkg, router, sum(sizes), nb * max_lines, comm=comm)
 
