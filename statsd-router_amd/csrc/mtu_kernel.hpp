@@ -178,25 +178,35 @@ __device__ __forceinline__ void mtu_load_tile(const MtuParams &p, uint32_t r0, u
     }
 }
 
-// LDS of the sort kernels: (nds + 1) counters, sized at launch (dynamic), so that small downstream
-// counts do not cap the resident waves
-__global__ __launch_bounds__(64) void mtu_count_kernel(MtuLaunch L) {
-    extern __shared__ uint32_t hist[];
-    const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.tile0; });
+// The sort kernels run one record tile per wave, kMtuSortWaves tiles per workgroup (fewer, larger
+// workgroups: a launch of 64-thread workgroups was dispatch-bound). Each wave has its own (nds + 1)
+// counters of dynamic LDS and syncs only with itself.
+constexpr int kMtuSortWaves = 4;
+__device__ __forceinline__ void mtu_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_count_kernel(MtuLaunch L) {
+    extern __shared__ uint32_t lds_hist[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t g = blockIdx.x * kMtuSortWaves + (uint32_t)wave;   // the wave's tile in the launch
+    if (g >= L.tiles) return;
+    const uint32_t bi = mtu_batch_of(L, g, [](const MtuBatchArg &a) { return a.tile0; });
     const MtuParams p = mtu_view(L, bi);
-    const int lane = threadIdx.x;
-    const uint32_t nk = p.nds + 1, t = blockIdx.x - L.b[bi].tile0;
+    const uint32_t nk = p.nds + 1, t = g - L.b[bi].tile0;
+    uint32_t *hist = lds_hist + (size_t)wave * nk;
     const uint32_t n = mtu_lines(p), r0 = t * kMtuTile;
     sr_record r[kMtuPerLane];
     if (r0 < n) mtu_load_tile(p, r0, n, lane, r);
     for (uint32_t k = lane; k < nk; k += 64) hist[k] = 0;
-    __syncthreads();
+    mtu_wave_sync();
     if (r0 < n) {
 #pragma unroll
         for (int k = 0; k < kMtuPerLane; ++k)
             if (r0 + (uint32_t)(64 * k + lane) < n) atomicAdd(&hist[mtu_key(r[k], p.nds)], 1u);
     }
-    __syncthreads();
+    mtu_wave_sync();
     for (uint32_t k = lane; k < nk; k += 64) p.tile_counts[(size_t)k * p.ntiles + t] = hist[k];
 }
 
@@ -268,19 +278,22 @@ __global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuLaunch L) {
     }
 }
 
-__global__ __launch_bounds__(64) void mtu_scatter_kernel(MtuLaunch L) {
-    extern __shared__ uint32_t pos[];
-    volatile uint32_t *vpos = pos;
-    const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.tile0; });
+__global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_scatter_kernel(MtuLaunch L) {
+    extern __shared__ uint32_t lds_pos[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t g = blockIdx.x * kMtuSortWaves + (uint32_t)wave;
+    if (g >= L.tiles) return;
+    const uint32_t bi = mtu_batch_of(L, g, [](const MtuBatchArg &a) { return a.tile0; });
     const MtuParams p = mtu_view(L, bi);
-    const int lane = threadIdx.x;
-    const uint32_t nk = p.nds + 1, t = blockIdx.x - L.b[bi].tile0;
+    const uint32_t nk = p.nds + 1, t = g - L.b[bi].tile0;
+    uint32_t *pos = lds_pos + (size_t)wave * nk;
+    volatile uint32_t *vpos = pos;
     const uint32_t n = mtu_lines(p), r0 = t * kMtuTile;
     if (r0 >= n) return;
     sr_record rr[kMtuPerLane];
     mtu_load_tile(p, r0, n, lane, rr);
     for (uint32_t k = lane; k < nk; k += 64) pos[k] = p.tile_counts[(size_t)k * p.ntiles + t];
-    __syncthreads();
+    mtu_wave_sync();
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
     for (int ck = 0; ck < kMtuPerLane; ++ck) {

@@ -396,10 +396,19 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     L.chunk_pk = c->d_mtu_chunks + 3 * (size_t)chunks;
     L.table = c->d_mtu_table;
     L.nx = reinterpret_cast<uint8_t *>(c->d_mtu_table + (((size_t)c->mtu_chunks * kMtuX + 1) & ~(size_t)1));
-    const size_t sort_lds = (size_t)(nds + 1) * sizeof(uint32_t);
-    hipLaunchKernelGGL(mtu_count_kernel, dim3(tiles), dim3(64), sort_lds, c->stream, L);
+    const size_t sort_lds = (size_t)kMtuSortWaves * (nds + 1) * sizeof(uint32_t);
+    static bool sort_attr = false;   // up to 4 x 4097 counters: past the 64 KiB default
+    if (!sort_attr) {
+        (void)hipFuncSetAttribute((const void *)mtu_count_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  96 * 1024);
+        (void)hipFuncSetAttribute((const void *)mtu_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  96 * 1024);
+        sort_attr = true;
+    }
+    const uint32_t sort_blocks = (tiles + kMtuSortWaves - 1) / kMtuSortWaves;
+    hipLaunchKernelGGL(mtu_count_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
     hipLaunchKernelGGL(mtu_scan_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
-    hipLaunchKernelGGL(mtu_scatter_kernel, dim3(tiles), dim3(64), sort_lds, c->stream, L);
+    hipLaunchKernelGGL(mtu_scatter_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
     hipLaunchKernelGGL(mtu_table_kernel, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
     hipLaunchKernelGGL(mtu_chain_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
     hipLaunchKernelGGL(mtu_emit_kernel, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
