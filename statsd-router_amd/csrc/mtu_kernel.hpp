@@ -29,8 +29,8 @@
 //               possible incoming fill x in 0..1450: packets closed, last start, fill out;
 //   mtu_chain   one workgroup: per shard, the chunks' tables composed in order from fill_in
 //               (one table read per chunk), packet counts scanned into descriptor slots;
-//   mtu_emit    per chunk: walks its packet chain from its incoming fill (one wave, next() in
-//               registers by 64-line windows) and writes descriptors.
+//   mtu_emit    per chunk: its packet chain from its incoming fill, by hops of 16 packets
+//               (doubling) and then 16-packet walks in parallel, writing descriptors.
 // Integer/byte work, latency-light: no MFMA.
 #pragma once
 
@@ -52,7 +52,8 @@ constexpr uint16_t kMtuEnd = 0xFFFFu;
 constexpr int kMtuMaxBatches = 32;
 
 // Developer ablation mask for timing the chunk kernels' phases (tools/ab_mtu.sh; results are wrong
-// when set, never shipped): 1 doubling, 2 table fills, 4 emit walk, 8 next(), 16 prefix sums.
+// when set, never shipped): 1 doubling, 2 table fills, 4 emit walk, 8 next(), 16 prefix sums,
+// 32 the table kernel's store of next() for emit.
 #ifndef SR_MTU_SKIP
 #define SR_MTU_SKIP 0
 #endif
@@ -85,6 +86,7 @@ struct MtuLaunch {
     uint32_t *closed;                  // [nb][nds] packets closed per shard
     uint64_t *table;                   // [chunks][kMtuX]
     uint8_t *nx;                       // [chunks][kMtuChunk] next(i) - i per line (mtu_table -> mtu_emit)
+    uint64_t *dbg;                     // SR_MTU_STAMPS developer builds only: 8 timestamps per chunk
     MtuBatchArg b[kMtuMaxBatches];
 };
 static_assert(sizeof(MtuLaunch) < 3584, "kernel argument size");
@@ -163,6 +165,15 @@ __device__ __forceinline__ uint32_t mtu_key(const sr_record &r, uint32_t nds) {
 
 __device__ __forceinline__ bool mtu_dropped(const MtuParams &p, uint32_t s) {
     return p.probed_dead && ((p.probed_dead[s >> 6] >> (s & 63)) & 1ull);
+}
+
+// developer timeline (SR_MTU_STAMPS builds): s_memrealtime (100 MHz) at phase boundaries per chunk
+__device__ __forceinline__ void mtu_stamp(const MtuLaunch &L, uint32_t gc, int slot) {
+#ifdef SR_MTU_STAMPS
+    if (threadIdx.x == 0 && L.dbg) L.dbg[(size_t)gc * 8 + slot] = __builtin_amdgcn_s_memrealtime();
+#else
+    (void)L, (void)gc, (void)slot;
+#endif
 }
 
 // ---- sort: histogram, scan, stable scatter ----------------------------------------------------
@@ -325,9 +336,13 @@ struct MtuTableSmem {
     uint32_t P[kMtuChunk];      // inclusive prefix of the chunk's line lengths
     uint32_t ld[kMtuChunk];     // last packet start reached from here << 16 | packets closed on the way
 };
+constexpr int kMtuHop = 16;   // packets per anchor of the emit walk
 struct MtuEmitSmem {
     uint32_t P[kMtuChunk];
     alignas(16) uint8_t nx[kMtuChunk];   // next(i) - i (1 .. kMtuWindow - 1), 0 = none in the chunk
+    uint16_t J[kMtuChunk];               // kMtuHop packet starts ahead on the chain (kMtuEnd: it ends first)
+    uint16_t anchor[kMtuChunk / kMtuHop + 2];
+    uint32_t nanchor;
 };
 
 struct MtuChunk {
@@ -369,9 +384,10 @@ __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuCh
     const uint32_t base = (uint32_t)wave * (kMtuChunk / (kMtuBlock / 64)) + (uint32_t)lane;
     uint32_t v[kMtuPer];
 #pragma unroll
-    for (int k = 0; k < kMtuPer; ++k) {
+    for (int k = 0; k < kMtuPer; ++k) {   // unconditional (clamped) loads: all 16 in flight together
         const uint32_t i = base + 64u * k;
-        v[k] = i < ck.cnt ? p.sorted[ck.pos0 + i].length : 0u;
+        const uint32_t len = p.sorted[ck.pos0 + min(i, ck.cnt - 1)].length;
+        v[k] = i < ck.cnt ? len : 0u;
     }
     uint32_t carry = 0;
 #pragma unroll
@@ -398,20 +414,26 @@ __device__ __forceinline__ void mtu_chunk_next(const uint32_t *P, uint32_t cnt, 
         for (uint32_t i = threadIdx.x; i < cnt; i += kMtuBlock) f(i, i + 22 < cnt ? (uint16_t)(i + 22) : kMtuEnd);
         return;
     }
+    // (every LDS read unconditional, at a clamped index: a read under a per-lane condition became
+    // a branch with its own wait, and the 16 searches ran one after another)
     const uint32_t total = P[cnt - 1];
     uint32_t lo[kMtuPer], lim[kMtuPer];
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) {
         const uint32_t i = threadIdx.x + (uint32_t)k * kMtuBlock;
         lo[k] = i;   // P[i] <= lim: a line alone always fits
-        lim[k] = (i && i < cnt ? P[i - 1] : 0u) + (uint32_t)kMtuCap;
+        const uint32_t pm = P[min(i ? i - 1 : 0u, cnt - 1)];
+        lim[k] = pm * (uint32_t)(i != 0) + (uint32_t)kMtuCap;
     }
+    // past the chunk the clamped read gives P[cnt - 1] = total, which is over lim unless no line
+    // closes the packet (next = kMtuEnd below, lo unused): no bounds test, so no branch
 #pragma unroll
     for (uint32_t step = 128; step; step >>= 1) {
 #pragma unroll
         for (int k = 0; k < kMtuPer; ++k) {
             const uint32_t t = lo[k] + step;
-            if (t < cnt && P[t] <= lim[k]) lo[k] = t;
+            const uint32_t pt = P[min(t, cnt - 1)];
+            lo[k] = pt <= lim[k] ? t : lo[k];
         }
     }
 #pragma unroll
@@ -430,13 +452,17 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
     const uint32_t c = blockIdx.x - L.b[bi].chunk0;
     if (!mtu_chunk_of(p, c, ck)) return;
     const int tid = threadIdx.x;
+    mtu_stamp(L, blockIdx.x, 0);
     mtu_chunk_prefix(p, ck, sm.P, sm.ld);
+    mtu_stamp(L, blockIdx.x, 1);
     uint8_t *gnx = p.nx + (size_t)c * kMtuChunk;
     mtu_chunk_next(sm.P, ck.cnt, [&](uint32_t i, uint16_t nxt) {
         sm.ld[i] = nxt == kMtuEnd ? i << 16 : ((uint32_t)nxt << 16) | 1u;
-        gnx[i] = nxt == kMtuEnd ? 0 : (uint8_t)(nxt - i);   // for mtu_emit
+        if (!(SR_MTU_SKIP & 32)) gnx[i] = nxt == kMtuEnd ? 0 : (uint8_t)(nxt - i);   // for mtu_emit
     });
+    for (uint32_t i = ck.cnt + (uint32_t)tid; i < (uint32_t)kMtuChunk; i += kMtuBlock) sm.ld[i] = i << 16;   // self loops
     __syncthreads();
+    mtu_stamp(L, blockIdx.x, 2);
     const uint32_t total = sm.P[ck.cnt - 1];
     // pointer doubling: ld -> the last packet start of the chain and the packets closed on it.
     // A chain closes at most 2 * total / (cap + 1) + 1 packets (two consecutive closed packets
@@ -445,16 +471,17 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
     // In place, one barrier per round: a neighbour read mid-round has jumped at least as far as
     // at the round's start, so after r rounds every jump spans >= 2^r starts (or ends the chain).
     for (uint32_t span = 1; !(SR_MTU_SKIP & 1) && span < kb; span <<= 1) {
+        uint32_t v[kMtuPer], w[kMtuPer];   // every line (past the chunk: self loops), loads first
 #pragma unroll
-        for (int k = 0; k < kMtuPer; ++k) {
-            const uint32_t i = (uint32_t)tid + (uint32_t)k * kMtuBlock;
-            if (i < ck.cnt) {
-                const uint32_t v = sm.ld[i], w = sm.ld[v >> 16];
-                sm.ld[i] = (w & 0xFFFF0000u) | ((v + w) & 0xFFFFu);
-            }
-        }
+        for (int k = 0; k < kMtuPer; ++k) v[k] = sm.ld[(uint32_t)tid + (uint32_t)k * kMtuBlock];
+#pragma unroll
+        for (int k = 0; k < kMtuPer; ++k) w[k] = sm.ld[v[k] >> 16];
+#pragma unroll
+        for (int k = 0; k < kMtuPer; ++k)
+            sm.ld[(uint32_t)tid + (uint32_t)k * kMtuBlock] = (w[k] & 0xFFFF0000u) | ((v[k] + w[k]) & 0xFFFFu);
         __syncthreads();
     }
+    mtu_stamp(L, blockIdx.x, 3);
     // incoming fills x0 .. x0 + per - 1 per thread: the first line over the cap moves down with x
     constexpr uint32_t per = (kMtuX + kMtuBlock - 1) / kMtuBlock;
     const uint32_t hi = min(ck.cnt, (uint32_t)kMtuWindow);
@@ -479,6 +506,7 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
         }
         row[x] = e;
     }
+    mtu_stamp(L, blockIdx.x, 4);
 }
 
 // One workgroup: the chunks of every shard composed in order, descriptor slots scanned.
@@ -535,9 +563,10 @@ __device__ __forceinline__ void mtu_put(const MtuParams &p, uint32_t k, uint32_t
     }
 }
 
-// The chunk's packet chain (the first line that does not fit the incoming packet, then next())
-// is walked by one wave over 64-line windows of next() held in registers: each step is a lane
-// read, not an LDS round trip; the chain members of a window then write their descriptors.
+// The chunk's packet chain (the first line that does not fit the incoming packet, then next()):
+// four rounds of pointer doubling give every line the start kMtuHop packets ahead (J); one thread
+// walks the chain by those hops, leaving an anchor every kMtuHop packets; then every anchor's
+// thread walks its kMtuHop packets by next() and writes their descriptors (rank = 16 q + step).
 __global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuLaunch L) {
     __shared__ MtuEmitSmem sm;
     MtuChunk ck;
@@ -545,59 +574,76 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuLaunch L) {
     const MtuParams p = mtu_view(L, bi);
     const uint32_t c = blockIdx.x - L.b[bi].chunk0;
     if (!mtu_chunk_of(p, c, ck)) return;
+    mtu_stamp(L, blockIdx.x, 5);
+    const int tid = threadIdx.x;
     {   // next(i) - i as mtu_table stored it: 16 bytes per thread
         const uint4 *src = reinterpret_cast<const uint4 *>(p.nx + (size_t)c * kMtuChunk);
-        const uint32_t q = threadIdx.x;
-        const uint4 v = q * 16 < ck.cnt ? src[q] : make_uint4(0, 0, 0, 0);
-        mtu_chunk_prefix(p, ck, sm.P, reinterpret_cast<uint32_t *>(sm.nx));
-        reinterpret_cast<uint4 *>(sm.nx)[q] = v;
+        const uint4 v = (uint32_t)tid * 16 < ck.cnt ? src[tid] : make_uint4(0, 0, 0, 0);
+        mtu_chunk_prefix(p, ck, sm.P, reinterpret_cast<uint32_t *>(sm.J));
+        reinterpret_cast<uint4 *>(sm.nx)[tid] = v;
     }
     __syncthreads();
-    if (threadIdx.x >= 64) return;
-    const uint32_t lane = threadIdx.x;
+    mtu_stamp(L, blockIdx.x, 6);
     const uint32_t x = p.chunk_entry[c], open = p.chunk_open[c], k0 = p.chunk_pk[c];
     const uint32_t total = sm.P[ck.cnt - 1];
     const uint32_t carry = open == kMtuNone ? x : 0u;        // pending bytes from before the batch
     const uint32_t start = open == kMtuNone ? p.key_start[ck.shard] : open;
     if (x + total <= (uint32_t)kMtuCap) {   // no line of the chunk closes a packet: the incoming one stays open
-        if (ck.last && lane == 0)
+        if (ck.last && tid == 0)
             mtu_put(p, k0, start, ck.pos0 + ck.cnt - start, ck.shard, x - carry + total, carry, 1u);
         return;
     }
-    const uint32_t j = (uint32_t)__builtin_amdgcn_readfirstlane(
-        (int)mtu_first_over(sm.P, 0, min(ck.cnt, (uint32_t)kMtuWindow) - 1, (uint32_t)kMtuCap - x));
-    if (lane == 0)   // the incoming packet closes before line j
-        mtu_put(p, k0, start, ck.pos0 + j - start, ck.shard, x - carry + (j ? sm.P[j - 1] : 0u), carry, 0u);
-    const uint64_t lt = (1ull << lane) - 1ull;
-    uint32_t w = 0;
-    for (uint32_t base = j; !(SR_MTU_SKIP & 4);) {
-        const uint32_t a = base + lane;
-        const uint32_t d = a < ck.cnt ? (uint32_t)sm.nx[a] : 0u;
-        uint64_t mask = 0;
-        uint32_t off = 0;
-        bool done = false;
-        for (;;) {
-            mask |= 1ull << off;
-            const uint32_t dd = (uint32_t)__builtin_amdgcn_readlane((int)d, (int)off);
-            if (dd == 0) {
-                done = true;
-                break;
-            }
-            off += dd;
-            if (off >= 64) break;
+    // J: next(i), then doubled four times (exact: all reads of a round before its writes)
+    uint16_t jv[kMtuPer];
+#pragma unroll
+    for (int k = 0; k < kMtuPer; ++k) {
+        const uint32_t i = (uint32_t)tid + (uint32_t)k * kMtuBlock;
+        const uint32_t d = sm.nx[i];
+        jv[k] = (i < ck.cnt && d) ? (uint16_t)(i + d) : kMtuEnd;
+        sm.J[i] = jv[k];
+    }
+    __syncthreads();
+    for (int r = 0; !(SR_MTU_SKIP & 4) && (1 << r) < kMtuHop; ++r) {
+#pragma unroll
+        for (int k = 0; k < kMtuPer; ++k) {
+            const uint16_t t = sm.J[jv[k] == kMtuEnd ? 0u : jv[k]];
+            jv[k] = jv[k] == kMtuEnd ? kMtuEnd : t;
         }
-        if ((mask >> lane) & 1ull) {
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kMtuPer; ++k) sm.J[(uint32_t)tid + (uint32_t)k * kMtuBlock] = jv[k];
+        __syncthreads();
+    }
+    const uint32_t j = mtu_first_over(sm.P, 0, min(ck.cnt, (uint32_t)kMtuWindow) - 1, (uint32_t)kMtuCap - x);
+    if (tid == 0) {
+        // the incoming packet closes before line j; anchors every kMtuHop packet starts from j
+        mtu_put(p, k0, start, ck.pos0 + j - start, ck.shard, x - carry + (j ? sm.P[j - 1] : 0u), carry, 0u);
+        uint32_t n = 0;
+        for (uint32_t a = j; !(SR_MTU_SKIP & 4);) {
+            sm.anchor[n++] = (uint16_t)a;
+            const uint32_t nxt = sm.J[a];
+            if (nxt == kMtuEnd) break;
+            a = nxt;
+        }
+        sm.nanchor = n;
+    }
+    __syncthreads();
+    const uint32_t na = sm.nanchor;
+    for (uint32_t q = (uint32_t)tid; q < na; q += kMtuBlock) {
+        uint32_t a = sm.anchor[q], rank = q * kMtuHop;
+        for (int step = 0; step < kMtuHop; ++step, ++rank) {
+            const uint32_t d = sm.nx[a];
             const bool is_open = d == 0;   // the last packet start: the packet stays pending
             if (!is_open || ck.last) {     // else it continues into the next chunk
                 const uint32_t b = is_open ? ck.cnt : a + d;
-                mtu_put(p, k0 + 1 + w + (uint32_t)__popcll(mask & lt), ck.pos0 + a, b - a, ck.shard,
-                        sm.P[b - 1] - (a ? sm.P[a - 1] : 0u), 0u, is_open ? 1u : 0u);
+                mtu_put(p, k0 + 1 + rank, ck.pos0 + a, b - a, ck.shard, sm.P[b - 1] - (a ? sm.P[a - 1] : 0u), 0u,
+                        is_open ? 1u : 0u);
             }
+            if (is_open) break;
+            a += d;
         }
-        w += (uint32_t)__popcll(mask);
-        if (done) break;
-        base += off;
     }
+    mtu_stamp(L, blockIdx.x, 7);
 }
 
 }  // namespace srk

@@ -351,6 +351,16 @@ static int mtu_reserve(sr_ctx *c, uint32_t tiles, uint32_t chunks, uint32_t nb) 
     return 0;
 }
 
+#ifdef SR_MTU_STAMPS
+static uint64_t *g_mtu_dbg = nullptr;
+static size_t g_mtu_dbg_n = 0;
+extern "C" size_t sr_mtu_stamps(uint64_t *dst, size_t max_chunks) {
+    const size_t n = g_mtu_dbg_n < max_chunks ? g_mtu_dbg_n : max_chunks;
+    if (g_mtu_dbg && n) (void)hipMemcpy(dst, g_mtu_dbg, n * 8 * sizeof(uint64_t), hipMemcpyDeviceToHost);
+    return n;
+}
+#endif
+
 int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) {
     if (!c || !batches || count == 0 || count > (size_t)kMtuMaxBatches) return -EINVAL;
     const uint32_t nds = c->ds.nds;
@@ -396,6 +406,21 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     L.chunk_pk = c->d_mtu_chunks + 3 * (size_t)chunks;
     L.table = c->d_mtu_table;
     L.nx = reinterpret_cast<uint8_t *>(c->d_mtu_table + (((size_t)c->mtu_chunks * kMtuX + 1) & ~(size_t)1));
+#ifdef SR_MTU_STAMPS   // developer timeline: 8 stamps per chunk, read back with sr_mtu_stamps
+    static uint64_t *d_dbg = nullptr;
+    static size_t dbg_cap = 0;
+    if (chunks > dbg_cap) {
+        if (d_dbg) (void)hipFree(d_dbg);
+        dbg_cap = chunks;
+        if (hipMalloc(&d_dbg, dbg_cap * 8 * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+    }
+    (void)hipMemsetAsync(d_dbg, 0, (size_t)chunks * 8 * sizeof(uint64_t), c->stream);
+    L.dbg = d_dbg;
+    g_mtu_dbg = d_dbg;
+    g_mtu_dbg_n = chunks;
+#else
+    L.dbg = nullptr;
+#endif
     const size_t sort_lds = (size_t)kMtuSortWaves * (nds + 1) * sizeof(uint32_t);
     static bool sort_attr = false;   // up to 4 x 4097 counters: past the 64 KiB default
     if (!sort_attr) {
