@@ -178,14 +178,14 @@ __device__ __forceinline__ void mtu_stamp(const MtuLaunch &L, uint32_t gc, int s
 
 // ---- sort: histogram, scan, stable scatter ----------------------------------------------------
 // The tile's records, loaded up front (kMtuTile / 64 independent loads in flight per lane rather
-// than one round trip per 64 records); key nds + 1 for positions past the batch.
+// than one round trip per 64 records; the caller ignores positions past the batch, n > r0 >= 0).
 constexpr int kMtuPerLane = kMtuTile / 64;
 __device__ __forceinline__ void mtu_load_tile(const MtuParams &p, uint32_t r0, uint32_t n, int lane,
                                               sr_record (&r)[kMtuPerLane]) {
 #pragma unroll
-    for (int k = 0; k < kMtuPerLane; ++k) {
+    for (int k = 0; k < kMtuPerLane; ++k) {   // clamped, unconditional: the eight loads in flight together
         const uint32_t i = r0 + (uint32_t)(64 * k + lane);
-        r[k] = i < n ? p.recs[i] : sr_record{0, 0, 0};
+        r[k] = p.recs[min(i, n - 1)];
     }
 }
 
@@ -297,8 +297,7 @@ __global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_scatter_kernel(MtuLaun
     const uint32_t bi = mtu_batch_of(L, g, [](const MtuBatchArg &a) { return a.tile0; });
     const MtuParams p = mtu_view(L, bi);
     const uint32_t nk = p.nds + 1, t = g - L.b[bi].tile0;
-    uint32_t *pos = lds_pos + (size_t)wave * nk;
-    volatile uint32_t *vpos = pos;
+    uint32_t *pos = lds_pos + (size_t)wave * nk;   // (plain LDS accesses; the wave syncs below order them)
     const uint32_t n = mtu_lines(p), r0 = t * kMtuTile;
     if (r0 >= n) return;
     sr_record rr[kMtuPerLane];
@@ -306,25 +305,32 @@ __global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_scatter_kernel(MtuLaun
     for (uint32_t k = lane; k < nk; k += 64) pos[k] = p.tile_counts[(size_t)k * p.ntiles + t];
     mtu_wave_sync();
     const uint64_t lt = (1ull << lane) - 1ull;
+    // every key before the first store: the loads are waited for here, not inside the rank loops
+    // (a loop that stores cannot count its own stores, so a load first used inside it costs a
+    // wait for every store before it)
+    uint32_t keys[kMtuPerLane];
+#pragma unroll
+    for (int ck = 0; ck < kMtuPerLane; ++ck) keys[ck] = mtu_key(rr[ck], p.nds);
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the tile's records are in registers
 #pragma unroll
     for (int ck = 0; ck < kMtuPerLane; ++ck) {
         const uint32_t i = r0 + (uint32_t)(64 * ck + lane);
         bool pend = i < n;
         const sr_record r = rr[ck];
-        const uint32_t key = pend ? mtu_key(r, p.nds) : 0u;
+        const uint32_t key = keys[ck];
         // stable in-wave ranks: one round per distinct key of the 64 records
         for (uint64_t pm = __ballot(pend); pm; pm = __ballot(pend)) {
             const int leader = __builtin_ctzll(pm);
             const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)key, leader);
             const bool mine = pend && key == k0;
             const uint64_t m = __ballot(mine);
-            const uint32_t base = vpos[k0];
+            const uint32_t base = pos[k0];
             if (mine) {
                 p.sorted[base + (uint32_t)__popcll(m & lt)] = r;
                 pend = false;
             }
-            if (lane == leader) vpos[k0] = base + (uint32_t)__popcll(m);
-            __builtin_amdgcn_wave_barrier();
+            if (lane == leader) pos[k0] = base + (uint32_t)__popcll(m);
+            mtu_wave_sync();
         }
     }
 }
