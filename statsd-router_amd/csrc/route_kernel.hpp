@@ -499,27 +499,44 @@ __device__ __noinline__ void note_all_dead(uint64_t *pd, uint32_t n) {
 // visits (sr-main.c:106) are recorded by probed_dead_kernel, a replay after the launch: any extra
 // live value in this loop costs the route kernel a spill (measured: 9 % at C2, all alive).
 // MARK: when non-null, every dead shard visited is set in that bitmap (the replay's use).
+// The route kernel keeps the divisors' reciprocals its probes need first, N .. N - kMagicLds + 1,
+// in the padding dword of LDS image rows (entry e, word w at row 4 e + w; the rows' padding is
+// never read as bytes), so that a probe step waits on LDS rather than on a global load (a global
+// load waited for inside the line loop also waits for every record store before it).
+constexpr uint32_t kMagicLds = kOverlay + 1;
+__device__ __forceinline__ Magic magic_from_pad(const uint32_t *img, uint32_t e) {
+    Magic mg;
+    const uint32_t lo = img[(4 * e) * 17 + 16], hi = img[(4 * e + 1) * 17 + 16];
+    mg.m = ((uint64_t)hi << 32) | lo;
+    mg.shift = img[(4 * e + 2) * 17 + 16];
+    mg.kind = img[(4 * e + 3) * 17 + 16];
+    return mg;
+}
+
 template <bool MARK = false>
-__device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark = nullptr) {
+__device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark = nullptr,
+                                const uint32_t *pad_img = nullptr) {
     const uint32_t n = p.nds;
     if (p.dead >= n) {                                    // includes N == 0
         if (MARK && n) note_all_dead(mark, n);
         return SR_ROUTE_ALL_DEAD;
     }
     if (p.dead == 0) return mod_magic(h, p.magic_n, n);   // every shard alive: j = h % N
+    // up to 64 shards the alive bitmap is one word, read once per probe
+    const uint64_t alive0 = n <= 64 ? p.alive[0] : 0ull;
     // ds_index[] is the identity plus an overlay of (position -> value) writes, newest last.
     uint32_t ov[kOverlay];   // (pos << 16) | value
     int nov = 0;
 #pragma unroll
     for (int e = 0; e < kOverlay; ++e) ov[e] = 0xFFFFFFFFu;
     for (uint32_t i = n; i > 0; --i) {
-        const Magic mg = p.magic[i];
+        const Magic mg = (pad_img && n - i < kMagicLds) ? magic_from_pad(pad_img, n - i) : p.magic[i];
         const uint32_t j = mod_magic(h, mg, i);                      // :98
         uint32_t k = j;                                              // :99
 #pragma unroll
         for (int e = 0; e < kOverlay; ++e)
             if ((ov[e] >> 16) == j) k = ov[e] & 0xFFFFu;
-        if (alive_bit(p.alive, k)) return k;                         // :101-104
+        if (n <= 64 ? ((alive0 >> k) & 1ull) != 0 : alive_bit(p.alive, k)) return k;   // :101-104
         if (MARK) note_dead(mark, k);                                // :106
         if (j != i - 1) {                                            // :108-111
             uint32_t v = i - 1;
@@ -1320,7 +1337,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 uint32_t route;
                 if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
                 else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
-                else route = probe_shard(h, p);                                                    // :145
+                else route = probe_shard(h, p, nullptr, sm.img);                                   // :145
                 sr_record r;
                 r.offset = (uint32_t)(T0 + s);
                 r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
@@ -1591,6 +1608,10 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     in.sx = (ABL & ABL_AGENT_GRANULES) ? 0ull
                                        : __hip_atomic_load(&p.ctl->scan_xcc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < S::kPowWords) ((uint32_t *)&sm.kp_lo[0])[tid] = kp;   // kp_lo | kp_hi | kp_inv are contiguous
+    if (p.dead && p.dead < p.nds && tid < 4 * (int)kMagicLds) {   // the probe's first reciprocals (probe_shard)
+        const uint32_t e = (uint32_t)tid >> 2;   // divisor nds - e >= 1: entries e < nds only
+        if (e < p.nds) sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)&p.magic[p.nds - e])[tid & 3];
+    }
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
     uint64_t nlm, clm;
     uint32_t c_in;
