@@ -524,19 +524,38 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark
     if (p.dead == 0) return mod_magic(h, p.magic_n, n);   // every shard alive: j = h % N
     // up to 64 shards the alive bitmap is one word, read once per probe
     const uint64_t alive0 = n <= 64 ? p.alive[0] : 0ull;
-    // ds_index[] is the identity plus an overlay of (position -> value) writes, newest last.
-    uint32_t ov[kOverlay];   // (pos << 16) | value
-    int nov = 0;
+    auto alive_k = [&](uint32_t k) { return n <= 64 ? ((alive0 >> k) & 1ull) != 0 : alive_bit(p.alive, k); };
+    auto magic_i = [&](uint32_t i) {
+        return (pad_img && n - i < kMagicLds) ? magic_from_pad(pad_img, n - i) : p.magic[i];
+    };
+    // ds_index[] is the identity plus an overlay of (position -> value) writes, newest last. The
+    // first two picks see at most one overlay entry (kept in one register, o0): with few dead
+    // shards nearly every line ends there, without scanning the 16-entry overlay.
+    uint32_t o0 = 0xFFFFFFFFu, o1 = 0xFFFFFFFFu;   // (pos << 16) | value
+    uint32_t i = n;
+    for (int it = 0; it < 2 && i > 0; ++it, --i) {
+        const uint32_t j = mod_magic(h, magic_i(i), i);                                  // :98
+        const uint32_t k = (o0 >> 16) == j ? (o0 & 0xFFFFu) : j;                         // :99
+        if (alive_k(k)) return k;                                                         // :101-104
+        if (MARK) note_dead(mark, k);                                                     // :106
+        if (j != i - 1) {                                                                 // :108-111
+            const uint32_t v = (o0 >> 16) == i - 1 ? (o0 & 0xFFFFu) : i - 1;
+            if (o0 == 0xFFFFFFFFu) o0 = (j << 16) | v;
+            else o1 = (j << 16) | v;
+        }
+        h = (h * 7 + 5) / 3;                                                              // :113
+    }
+    uint32_t ov[kOverlay];
+    int nov = (o0 != 0xFFFFFFFFu) + (o1 != 0xFFFFFFFFu);
 #pragma unroll
-    for (int e = 0; e < kOverlay; ++e) ov[e] = 0xFFFFFFFFu;
-    for (uint32_t i = n; i > 0; --i) {
-        const Magic mg = (pad_img && n - i < kMagicLds) ? magic_from_pad(pad_img, n - i) : p.magic[i];
-        const uint32_t j = mod_magic(h, mg, i);                      // :98
+    for (int e = 0; e < kOverlay; ++e) ov[e] = e == 0 ? o0 : (e == 1 ? o1 : 0xFFFFFFFFu);
+    for (; i > 0; --i) {
+        const uint32_t j = mod_magic(h, magic_i(i), i);              // :98
         uint32_t k = j;                                              // :99
 #pragma unroll
         for (int e = 0; e < kOverlay; ++e)
             if ((ov[e] >> 16) == j) k = ov[e] & 0xFFFFu;
-        if (n <= 64 ? ((alive0 >> k) & 1ull) != 0 : alive_bit(p.alive, k)) return k;   // :101-104
+        if (alive_k(k)) return k;                                    // :101-104
         if (MARK) note_dead(mark, k);                                // :106
         if (j != i - 1) {                                            // :108-111
             uint32_t v = i - 1;
