@@ -55,9 +55,6 @@ struct sr_ctx {
 
 static void free_ptr(void *p) { (void)hipFree(p); }
 
-// The product launches exactly one instantiation, ABL_NONE. Ablation variants (records wrong by
-// design in some of them) exist only in builds made with -DSR_ABLATION_VARIANTS (`make VARIANTS=1`,
-// developer A/B runs; never the shipped library): SR_VARIANT in the environment then selects one.
 // The product launches KV_UNIFORM or KV_SEGMENTS (identical records; DeviceState::choose_segments
 // picks by the lane-layout policy). Ablation variants (records wrong by design in some of them)
 // exist only in builds made with -DSR_ABLATION_VARIANTS (`make VARIANTS=1`, developer A/B runs;
