@@ -131,8 +131,9 @@ def main(argv=None):
     if rc is not None:
         sys.exit(rc)
     if args.dry_ranks:
-        print(json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")}),
-              flush=True)
+        # one write(2) per rank: the ranks share the pipe, and a short write is atomic on it
+        line = json.dumps({k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR")})
+        os.write(1, (line + "\n").encode())
         return
 
     import numpy as np
