@@ -1132,8 +1132,14 @@ __device__ __forceinline__ void tile_issue(const RouteParams &p, uint32_t bi, ui
     in.hv = make_uint4(0, 0, 0, 0);
     if (tid < kHalo / 16 && t > 0 && !(ABL & ABL_NO_PROLOGUE))   // zeros before the batch start
         in.hv = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, T0 - kHalo + tid * 16, 0, 0));
+    if (T0 + (uint32_t)kTileB <= bd.nbytes) {   // every tile but a batch's last: no per-piece bounds test
 #pragma unroll
-    for (int k = 0; k < 4; ++k) in.v[k] = load16(rsrc, T0 + tid * kLaneBytes + k * 16, bd.nbytes);
+        for (int k = 0; k < 4; ++k)
+            in.v[k] = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, T0 + tid * kLaneBytes + k * 16, 0, 0));
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) in.v[k] = load16(rsrc, T0 + tid * kLaneBytes + k * 16, bd.nbytes);
+    }
 }
 
 // Route one tile (reference: sr-main.c:175-189 + process_data_line + hash + find_downstream's
@@ -1445,15 +1451,14 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
             // of mixed lengths (C5: a 64-byte line next to 1024-byte ones) gets one lane per
             // 64-byte name segment instead, the lines packed back to back over the lanes: no idle
             // lanes, one segment per lane.
-            bool segs = false, U2 = false;   // segment layout; lane units of two segments
+            bool segs = false;               // segment layout
             bool gain2 = false;              // the segment layout saves two or more rounds
             uint32_t TL = 0;                  // lanes the segment layout needs
             // (the segment variant decides in a tile's last window, after which the lane masks and
             // line states of later windows are dead)
             const bool last_win = wbase + kWin >= (int)tile_count;
             if ((ABL & KV_SEGMENTS) && last_win) {
-                // per line: 64-byte name segments, and lane units of one or two segments (two
-                // when one-segment units would take a second round of lanes)
+                // per line: 64-byte name segments, one lane each (an empty name still takes one)
                 uint32_t want = 0, nsg = 0;
                 if (tid < nwin) {
                     const int jj = tid, j = wbase + jj;
@@ -1464,7 +1469,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     const int len = e - s + 1;
                     if (len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH && c != kNone && c < e)
                         nsg = (uint32_t)(c - s + 63) >> 6;
-                    want = max(1u, nsg) | (max(1u, (nsg + 1) >> 1) << 16);
+                    want = max(1u, nsg);
                 }
                 const uint32_t incl = wave_incl_add32(want);
                 const uint32_t wmx = wave_incl_max32(nsg);
@@ -1482,23 +1487,23 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     pre += w < wave ? v : 0u;
                     mx = max(mx, sm.seg_w[w][1]);
                 }
-                tot = __builtin_amdgcn_readfirstlane(tot);
-                U2 = (tot & 0xFFFFu) > (uint32_t)BLOCK;
-                const int sh = U2 ? 16 : 0;
-                TL = (tot >> sh) & 0xFFFFu;
+                TL = __builtin_amdgcn_readfirstlane(tot);
                 // rounds of lanes times segments per lane, either way; the statistics for the
-                // host's choice of kernel count only the tiles that gain two or more
+                // host's choice of kernel count only the tiles that gain two or more. (A tile's
+                // segments exceed its 256 lanes by a few about half the time (C5): the second round
+                // then runs on the one or two waves that hold those segments, the others only meet
+                // its barriers; two-segment lanes everywhere cost 3 waves x 2 segments instead.)
                 const uint32_t mxs = (uint32_t)__builtin_amdgcn_readfirstlane(mx);
                 const int cost_u = ((nwin * G + BLOCK - 1) / BLOCK) * (int)((mxs + (uint32_t)G - 1) / (uint32_t)G);
-                const int cost_s = (((int)TL + BLOCK - 1) / BLOCK) * (U2 ? 2 : 1);
+                const int cost_s = ((int)TL + BLOCK - 1) / BLOCK;
                 segs = cost_s < cost_u;
                 gain2 = cost_s + 2 <= cost_u;
                 if (segs) {
                     // line starts as bits of a lane bitmap; per 64-lane word, the line covering
                     // its first lane and where that line starts
                     if (tid < nwin) {
-                        const uint32_t wn = (want >> sh) & 0xFFFFu;
-                        const uint32_t st = ((pre + incl - want) >> sh) & 0xFFFFu;
+                        const uint32_t wn = want;
+                        const uint32_t st = pre + incl - want;
                         atomicOr(&sm.seg_mask[st >> 6], 1ull << (st & 63));
                         const uint32_t m = (st + 63) & ~63u;
                         if (m < st + wn) sm.seg_first[m >> 6] = (st << 16) | (uint32_t)tid;
@@ -1523,44 +1528,47 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     const uint32_t x = (uint32_t)(r0 + tid);
                     const uint32_t k = x >> 6;   // the lane word: wave-uniform
                     const bool act = x < TL;
-                    const uint64_t mask = readlane64(act ? sm.seg_mask[k] : 0ull, 0);
-                    const uint32_t fst = (uint32_t)__builtin_amdgcn_readfirstlane(act ? sm.seg_first[k] : 0u);
-                    const uint64_t below = mask & (~0ull >> (63 - lane));
-                    const int hb = below ? 63 - __clzll(below) : -1;   // head lane of my line here
-                    const int jj = (int)(fst & 0xFFFFu) + __popcll(below) - (int)(mask & 1ull);
-                    const int sg = below ? lane - hb : (int)(x - (fst >> 16));   // my segment of the line
-                    const int j = wbase + jj;
-                    const int e = act ? sm.lend[jj + 1] : 0;
-                    int c = act ? sm.lcol[jj + 1] : kNone;
-                    if (j == 0 && c_pre != kNone) c = c_pre;
-                    const int s = (j == 0) ? s_pre : (act ? sm.lend[jj] + 1 : 0);
-                    const int len = e - s + 1;
-                    const bool len_ok = len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH;   // :180
-                    const bool fmt_ok = c != kNone && c < e;                                                // :140
-                    const int n = c - s;
-                    const int nseg = (act && len_ok && fmt_ok) ? (n + 63) >> 6 : 0;   // 0: an empty name
-                    const int glast = max(U2 ? (nseg + 1) >> 1 : nseg, 1) - 1;          // the line's last lane
-                    uint64_t hs = 0;
-                    for (int kk = 0; kk <= (int)U2; ++kk) {   // my unit: segments (U2 + 1) sg + kk
-                        const int kq = (U2 ? 2 * sg : sg) + kk;
-                        if (kq < nseg) {
-                            const int a = s + 64 * kq, nn = min(64, n - 64 * kq);
-                            const bool mid = !have_base && kq == nseg - 1;
-                            uint64_t hq = sdbm_img(sm, a + kHalo, nn, mid ? base_slot : nullptr, &st_early);
-                            if (kq + 1 < nseg) hq *= kpow_n(sm, c - a - nn);
-                            hs += hq;
+                    // a wave without a segment in this round only meets the barrier
+                    const bool live = r0 + wave * 64 < (int)TL;
+                    uint64_t below = 0, part = 0;
+                    int sg = 0, glast = -1, j = 0, s = 0, len = 0;
+                    bool len_ok = false, fmt_ok = false;
+                    if (live) {
+                        const uint64_t mask = readlane64(act ? sm.seg_mask[k] : 0ull, 0);
+                        const uint32_t fst = (uint32_t)__builtin_amdgcn_readfirstlane(act ? sm.seg_first[k] : 0u);
+                        below = mask & (~0ull >> (63 - lane));
+                        const int hb = below ? 63 - __clzll(below) : -1;   // head lane of my line here
+                        const int jj = (int)(fst & 0xFFFFu) + __popcll(below) - (int)(mask & 1ull);
+                        sg = below ? lane - hb : (int)(x - (fst >> 16));   // my segment of the line
+                        j = wbase + jj;
+                        const int e = act ? sm.lend[jj + 1] : 0;
+                        int c = act ? sm.lcol[jj + 1] : kNone;
+                        if (j == 0 && c_pre != kNone) c = c_pre;
+                        s = (j == 0) ? s_pre : (act ? sm.lend[jj] + 1 : 0);
+                        len = e - s + 1;
+                        len_ok = len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH;   // :180
+                        fmt_ok = c != kNone && c < e;                                                // :140
+                        const int n = c - s;
+                        const int nseg = (act && len_ok && fmt_ok) ? (n + 63) >> 6 : 0;   // 0: an empty name
+                        glast = act ? max(nseg, 1) - 1 : -1;                              // the line's last lane
+                        uint64_t hs = 0;
+                        if (sg < nseg) {
+                            const int a = s + 64 * sg, nn = min(64, n - 64 * sg);
+                            const bool mid = !have_base && sg == nseg - 1;
+                            hs = sdbm_img(sm, a + kHalo, nn, mid ? base_slot : nullptr, &st_early);
+                            if (sg + 1 < nseg) hs *= kpow_n(sm, c - a - nn);
                         }
+                        // a line's sum from the inclusive wave scan: S(x) - S(head - 1), or S(x) plus
+                        // the line's part in the previous word (a line spans at most 23 lanes)
+                        const uint64_t S = wave_scan64(hs, 0ull, [](uint64_t l, uint64_t r) { return l + r; });
+                        const int src = hb > 0 ? hb - 1 : 0;
+                        const uint64_t Sb = ((uint64_t)(uint32_t)__shfl((int)(S >> 32), src, 64) << 32) |
+                                            (uint32_t)__shfl((int)(uint32_t)S, src, 64);
+                        part = hb > 0 ? S - Sb : S;
+                        if (lane == 63 && act && sg < glast) sm.seg_carry[k] = part;   // continues in word k + 1
                     }
-                    // a line's sum from the inclusive wave scan: S(x) - S(head - 1), or S(x) plus
-                    // the line's part in the previous word (a line spans at most 23 lanes)
-                    const uint64_t S = wave_scan64(hs, 0ull, [](uint64_t l, uint64_t r) { return l + r; });
-                    const int src = hb > 0 ? hb - 1 : 0;
-                    const uint64_t Sb = ((uint64_t)(uint32_t)__shfl((int)(S >> 32), src, 64) << 32) |
-                                        (uint32_t)__shfl((int)(uint32_t)S, src, 64);
-                    const uint64_t part = hb > 0 ? S - Sb : S;
-                    if (lane == 63 && act && sg < glast) sm.seg_carry[k] = part;   // continues in word k + 1
                     wg_barrier();
-                    if (act && sg == glast) {
+                    if (sg == glast) {
                         const uint64_t h = below ? part : part + sm.seg_carry[k - 1];
                         finish(j, s, len, len_ok, fmt_ok, h);
                     }
