@@ -693,7 +693,10 @@ __device__ __forceinline__ uint64_t sdbm_img(const S &sm, int a, int n, const ui
     const int dw = a >> 2, s16 = dw & 15, cross = 16 - s16;
     const uint32_t *const p = &sm.img[(dw >> 4) * 17 + s16];
     const uint32_t first = p[0] & (0xFFFFFFFFu << (8 * lead));
-    if (F == 0) return sdbm_dword_fast(0, first & ((1u << (8 * rem)) - 1u)) * sm.kp_inv[4 - rem];
+    // a partial last dword of rem bytes: shifted up so that they are its high bytes (the bytes
+    // past the name drop out, and leading zero bytes leave a Horner value unchanged), then
+    // h K^rem + Horner(x): no mask and no K^-z correction
+    if (F == 0) return sdbm_dword_fast(0, first << (8 * (4 - rem)));
     uint64_t h = sdbm_dword_fast(0, first);
     int m = 1;
     // four dwords per iteration (a quarter of the loop control; adjacent reads pair into ds_read2)
@@ -705,7 +708,7 @@ __device__ __forceinline__ uint64_t sdbm_img(const S &sm, int a, int n, const ui
     for (; m + 3 < F; m += 4)
         h = sdbm_qword_fast(sdbm_qword_fast(h, p[m + 1], p[m + 2]), p[m + 3], p[m + 4]);
     for (; m < F; ++m) h = sdbm_dword_fast(h, p[m + 1]);
-    if (rem) h = sdbm_dword_fast(h, p[m + (m >= cross ? 1 : 0)] & ((1u << (8 * rem)) - 1u)) * sm.kp_inv[4 - rem];
+    if (rem) h = h * sm.kp_lo[rem] + sdbm_dword_fast(0, p[m + (m >= cross ? 1 : 0)] << (8 * (4 - rem)));
     return h;
 }
 
