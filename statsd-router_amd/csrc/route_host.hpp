@@ -50,7 +50,6 @@ struct DeviceState {
     uint32_t nds = 0, nwords = 0, dead = 0, max_tiles = 0, pending_cap = 0;
     size_t max_batch = 0;
     Magic magic_n{0, 0, 0};
-    Magic magic_n1{0, 0, 0};
     uint64_t *h_alive = nullptr;
     uint64_t *d_alive = nullptr;
     Magic *d_magic = nullptr;
@@ -103,7 +102,6 @@ struct DeviceState {
                 if (host_div(nn, mg[d]) != nn / d) return -EIO;
         }
         magic_n = n_downstreams ? mg[n_downstreams] : Magic{0, 0, 0};
-        magic_n1 = n_downstreams > 1 ? mg[n_downstreams - 1] : Magic{0, 0, 0};
         if (hipMemcpy(d_magic, mg.data(), mg.size() * sizeof(Magic), hipMemcpyHostToDevice) != hipSuccess)
             return -EIO;
         std::vector<uint64_t> kp(kPowLo + kPowHi + kPowInv);
@@ -174,7 +172,6 @@ struct DeviceState {
         p.dead = dead;
         p.pending_cap = pending_cap;
         p.magic_n = magic_n;
-        p.magic_n1 = magic_n1;
         p.alive = d_alive;
         p.magic = d_magic;
         p.kpow = d_kpow;

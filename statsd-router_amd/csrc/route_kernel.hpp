@@ -160,8 +160,7 @@ struct RouteParams {
     uint32_t nds;            // number of downstreams
     uint32_t dead;           // dead downstreams in the alive snapshot
     uint32_t pending_cap;
-    Magic magic_n;           // for h % nds (fast path, and the probe's first pick)
-    Magic magic_n1;          // for h % (nds - 1): the probe's second pick
+    Magic magic_n;           // for h % nds (fast path)
     const uint64_t *alive;   // bitmap
     const Magic *magic;      // [0..nds], index i -> divisor i
     const uint64_t *kpow;    // kPowLo + kPowHi + kPowInv entries: K^i (i < 64), K^(64 i) (i < 24), K^-z (z < 4)
@@ -564,8 +563,7 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark
     uint32_t o0 = 0xFFFFFFFFu, o1 = 0xFFFFFFFFu;   // (pos << 16) | value
     uint32_t i = n;
     for (int it = 0; it < 2 && i > 0; ++it, --i) {
-        // the first two divisors are wave-uniform: their reciprocals come with the kernel arguments
-        const uint32_t j = mod_magic(h, it == 0 ? p.magic_n : p.magic_n1, i);            // :98
+        const uint32_t j = mod_magic(h, magic_i(i), i);                                  // :98
         const uint32_t k = (o0 >> 16) == j ? (o0 & 0xFFFFu) : j;                         // :99
         if (alive_k(k)) return k;                                                         // :101-104
         if (MARK) note_dead(mark, k);                                                     // :106
