@@ -171,11 +171,17 @@ class LaunchRegrouper:
 
     def __call__(self, batches):
         """batches = [(d_bytes, nbytes, d_recs, max_records, d_n_records), ...] routed on the router's
-        stream. Returns (recv_bytes, recv_recs (offsets into recv_bytes), recv_counts [G, 2])."""
+        stream. Returns (recv_bytes, recv_recs (offsets into recv_bytes), recv_counts [G, 2]).
+
+        torch.distributed exchange: the collectives are ordered after torch's current stream, so the
+        router must launch on it. C-ABI exchange (comm): pack, sizes, sends, receives and rebase are
+        all ordered on the router's own stream, which need not be torch's current one; the returned
+        buffers are allocated for that stream and are ready once it has reached this point."""
         h = getattr(self.router, "stream_handle", 0)
-        if h == 0 or h != torch.cuda.current_stream().cuda_stream:
-            raise RuntimeError("LaunchRegrouper: router.set_stream(s.cuda_stream) with s = torch's current stream "
-                               "(a non-default stream) is required")
+        cur = torch.cuda.current_stream(self.bytes.device).cuda_stream
+        if h == 0 or (self.comm is None and h != cur):
+            raise RuntimeError("LaunchRegrouper: router.set_stream(s.cuda_stream) with s a non-default stream is "
+                               "required (for the torch.distributed exchange: torch's current stream)")
         if sum(b[3] for b in batches) > self.max_records or self.pkg.pack_capacity(sum(b[1] for b in batches)) > self.cap:
             raise ValueError("launch larger than the regrouper's buffers")
         self.router.pack_many_by_owner(batches, self.G, self.bytes.data_ptr(), self.cap, self.recs.data_ptr(),
@@ -183,12 +189,15 @@ class LaunchRegrouper:
         if self.comm is None:
             rb, rr, rc, self.last_sent, self.last_received = _exchange(self.bytes, self.recs, self.counts, self.group)
             return rb, rr, rc
-        # the C ABI: one size exchange (one host round trip), then the grouped sends and the rebase
-        rc = torch.empty((self.G, 2), dtype=torch.int64, device=self.bytes.device)
-        sent, received = self.router.exchange_sizes(self.comm, self.counts.data_ptr(), rc.data_ptr())
-        n_l, n_b = int(received[:, 0].sum()), int(received[:, 1].sum())
-        rb = torch.empty(max(n_b, 1), dtype=torch.uint8, device=self.bytes.device)
-        rr = torch.empty(max(n_l, 1), dtype=torch.int64, device=self.bytes.device)
+        # the C ABI: one size exchange (one host round trip), then the grouped sends and the rebase;
+        # receive buffers from the caching allocator's pool of the router's stream
+        rs = torch.cuda.ExternalStream(h, device=self.bytes.device) if h != cur else torch.cuda.current_stream()
+        with torch.cuda.stream(rs):
+            rc = torch.empty((self.G, 2), dtype=torch.int64, device=self.bytes.device)
+            sent, received = self.router.exchange_sizes(self.comm, self.counts.data_ptr(), rc.data_ptr())
+            n_l, n_b = int(received[:, 0].sum()), int(received[:, 1].sum())
+            rb = torch.empty(max(n_b, 1), dtype=torch.uint8, device=self.bytes.device)
+            rr = torch.empty(max(n_l, 1), dtype=torch.int64, device=self.bytes.device)
         self.router.exchange_data(self.comm, self.bytes.data_ptr(), self.recs.data_ptr(), sent, received,
                                   rb.data_ptr(), rr.data_ptr())
         self.last_sent, self.last_received = sent.astype(np.int64).tolist(), received.astype(np.int64).tolist()

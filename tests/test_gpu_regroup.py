@@ -219,6 +219,22 @@ def test_launch_regrouper_c_exchange(pkg, oracle, torch_stream):
                 rb, rr, rc = reg(batches)
                 torch.cuda.synchronize()
                 out[name] = (rb.cpu().numpy(), rr.cpu().numpy(), rc.cpu().numpy().tolist(), reg.last_received)
+            # the C exchange orders itself on the router's stream: a router on another stream than
+            # torch's current one is accepted there (the torch.distributed path refuses it)
+            other = torch.cuda.Stream()
+            r.set_stream(other.cuda_stream)
+            d_rec.zero_()
+            torch.cuda.synchronize()
+            r.route_device_many([(db, nb, dr, mr, None, dn) for db, nb, dr, mr, dn in batches])
+            with pytest.raises(RuntimeError):
+                rg.LaunchRegrouper(pkg, r, total, 4 * cap)(batches)
+            reg = rg.LaunchRegrouper(pkg, r, total, 4 * cap, comm=comm)
+            rb, rr, rc = reg(batches)
+            other.synchronize()
+            out["c_other_stream"] = (rb.cpu().numpy(), rr.cpu().numpy(), rc.cpu().numpy().tolist(), reg.last_received)
+        assert np.array_equal(out["c"][0], out["c_other_stream"][0])
+        assert np.array_equal(out["c"][1], out["c_other_stream"][1])
+        assert out["c"][2] == out["c_other_stream"][2] and out["c"][3] == out["c_other_stream"][3]
         assert np.array_equal(out["torch"][0], out["c"][0])
         assert np.array_equal(out["torch"][1], out["c"][1])
         assert out["torch"][2] == out["c"][2] and out["torch"][3] == out["c"][3]
