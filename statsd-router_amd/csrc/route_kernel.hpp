@@ -627,7 +627,7 @@ struct SmemT {
     uint64_t seg_mask[kSegWords];
     uint32_t seg_first[kSegWords];
     uint64_t seg_carry[kSegWords];
-    uint32_t wave_scan[kWaves][4];   // per wave, inclusive at its last lane: '\n' count, latest '\n' lane, colon key
+    uint32_t wave_scan[kWaves][4];   // per wave, inclusive at its last lane: '\n' count, 1 + latest '\n' position, colon key; a chunk with two '\n'
     uint64_t kp_lo[kPowLo];          // K^i
     uint64_t kp_hi[kPowHi];          // K^(64 i)
     uint64_t kp_inv[kPowInv];        // K^-z (an LDS read rather than three 64-bit constants held in VGPRs)
@@ -1264,11 +1264,16 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
     };
     const uint32_t l_in = wave_incl_max32(nlm ? (uint32_t)tid + 1u : 0u);
     const uint32_t k_in = wave_incl_min32(((uint32_t)(BLOCK - (int)l_in) << 17) | lane_cand(nlm, clm));
-    if (lane == 63) *(uint4 *)&sm.wave_scan[wave][0] = make_uint4(c_in, l_in, k_in, 0u);
+    // one '\n' at most in every chunk of the wave (the one-line-per-lane path below)
+    const uint32_t multi = __ballot(__popcll(nlm) > 1) != 0ull ? 1u : 0u;
+    if (lane == 63) *(uint4 *)&sm.wave_scan[wave][0] = make_uint4(c_in, l_in, k_in, multi);
     wg_barrier();
     stamp<ABL>(p, tid, g, 2);
     int lane_first, open_fc;
     lane_state(c_in, l_in, k_in, lane_first, open_fc);
+    uint32_t multi_any = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) multi_any |= sm.wave_scan[w][3];
 
     // ---- last wave: where the line that straddles into the tile starts, its first ':' ----------
     if (wave == kPreWave) {
@@ -1372,7 +1377,20 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
     bool have_base = (ABL & (ABL_NO_LOOKBACK | ABL_NO_LINES | ABL_FAKE_BASE)) != 0;
     // Window 0 is staged from the masks in registers; later windows (tiles of more than kWin lines)
     // recompute them from the LDS image, so that no mask or line state stays live through the hash.
-    if (tile_count > 0) stage(0, nlm, clm, lane_first, open_fc);
+    // A tile whose chunks hold one '\n' at most and whose lines fit one window (C2's shape) stages
+    // each line straight from its chunk: no loop over the chunk's '\n' bits.
+    if (tile_count > 0) {
+        if (!multi_any && (int)tile_count <= kWin) {
+            if (nlm) {
+                const int b = __builtin_ctzll(nlm);
+                const uint64_t cm = clm & (b == 0 ? 0ull : (~0ull >> (64 - b)));
+                sm.lend[lane_first + 1] = o + b;
+                sm.lcol[lane_first + 1] = open_fc != kNone ? open_fc : (cm ? o + __builtin_ctzll(cm) : kNone);
+            }
+        } else {
+            stage(0, nlm, clm, lane_first, open_fc);
+        }
+    }
     for (int wbase = 0; wbase < (int)tile_count;) {
         wg_barrier();
         if (wbase == 0) stamp<ABL>(p, tid, g, 4);
@@ -1421,12 +1439,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
             // 64-byte segments gi, gi + Gl, ...), shard, record. Gw: the wave-uniform bound of
             // the lane groups (groups are aligned to their size, so xor partners below Gl stay
             // inside the group).
-            auto line = [&](int jj, bool act, int gi, int Gl, int Gw) {
-                const int j = wbase + jj;
-                const int e = act ? sm.lend[jj + 1] : 0;
-                int c = act ? sm.lcol[jj + 1] : kNone;
-                if (j == 0 && c_pre != kNone) c = c_pre;   // the straddling line's ':' lies before T0
-                const int s = (j == 0) ? s_pre : (act ? sm.lend[jj] + 1 : 0);
+            auto line_at = [&](int j, int e, int c, int s, bool act, int gi, int Gl, int Gw) {
                 const int len = e - s + 1;
                 const bool len_ok = len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH;   // :180
                 const bool fmt_ok = c != kNone && c < e;                                                // :140
@@ -1448,6 +1461,14 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     if (d < Gl) h += v;
                 }
                 if (act && gi == 0) finish(j, s, len, len_ok, fmt_ok, h);
+            };
+            auto line = [&](int jj, bool act, int gi, int Gl, int Gw) {
+                const int j = wbase + jj;
+                const int e = act ? sm.lend[jj + 1] : 0;
+                int c = act ? sm.lcol[jj + 1] : kNone;
+                if (j == 0 && c_pre != kNone) c = c_pre;   // the straddling line's ':' lies before T0
+                const int s = (j == 0) ? s_pre : (act ? sm.lend[jj] + 1 : 0);
+                line_at(j, e, c, s, act, gi, Gl, Gw);
             };
             // Lanes per line. A tile whose longest name fits its G lanes in one pass (uniform
             // lengths: C2, C4) keeps one G-lane group per line (the KV_UNIFORM kernel always). A tile
