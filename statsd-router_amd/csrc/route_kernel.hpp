@@ -627,7 +627,7 @@ struct SmemT {
     uint64_t seg_mask[kSegWords];
     uint32_t seg_first[kSegWords];
     uint64_t seg_carry[kSegWords];
-    uint32_t wave_scan[kWaves][4];   // per wave, inclusive at its last lane: '\n' count, 1 + latest '\n' position, colon key; a chunk with two '\n'
+    uint32_t wave_scan[kWaves][4];   // per wave, inclusive at its last lane: '\n' count, -, colon key; a chunk with two '\n'
     uint64_t kp_lo[kPowLo];          // K^i
     uint64_t kp_hi[kPowHi];          // K^(64 i)
     uint64_t kp_inv[kPowInv];        // K^-z (an LDS read rather than three 64-bit constants held in VGPRs)
@@ -1232,8 +1232,9 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
     //  * the colon candidate of a chunk is its first ':' after its last '\n' (or its first ':' if it
     //    holds no '\n'): the first ':' of the line open at a chunk's end is the smallest candidate
     //    from the latest chunk with a '\n' on;
-    //  * key = ((BLOCK - L) << 17) | candidate, L = 1 + latest thread with a '\n' up to here (0: none
-    //    in this wave), so a min-scan of keys takes the smallest candidate of the latest segment.
+    //  * key = ((8191 - C) << 17) | candidate, C = the inclusive '\n' count of the wave up to here
+    //    (the same for every lane after the latest '\n', smaller before it), so a min-scan of keys
+    //    takes the smallest candidate of the latest segment.
     auto lane_cand = [&](uint64_t nl, uint64_t cl) -> uint32_t {
         uint64_t cm = cl;
         if (nl) {
@@ -1244,7 +1245,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
     };
     // the lane's first line and the first ':' of the line open at its start, from the inclusive
     // wave scans and the earlier waves' totals (sm.wave_scan)
-    auto lane_state = [&](uint32_t cin, uint32_t lin, uint32_t kin, int &lf, int &ofc) {
+    auto lane_state = [&](uint32_t cin, uint32_t kin, int &lf, int &ofc) {
         uint32_t p_cnt = 0, p_col = (uint32_t)kNone;   // the earlier waves: '\n' count, open line's first ':'
 #pragma unroll
         for (int w = 0; w < kWaves - 1; ++w) {
@@ -1252,25 +1253,23 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 const uint4 ws = *(const uint4 *)&sm.wave_scan[w][0];
                 p_cnt += ws.x;
                 const uint32_t wc = ws.z & 0x1FFFFu;
-                p_col = ws.y ? wc : min(p_col, wc);
+                p_col = ws.x ? wc : min(p_col, wc);
             }
         }
         // exclusive state of this lane: the inclusive state of the lane below, on top of the prefix
         const uint32_t c_ex = wave_shr1_32(cin, 0u);
-        const uint32_t l_ex = wave_shr1_32(lin, 0u);
         const uint32_t k_ex = wave_shr1_32(kin, 0xFFFFFFFFu) & 0x1FFFFu;
         lf = (int)(p_cnt + c_ex);                       // tile-local index of lane's 1st line
-        ofc = (int)(l_ex ? k_ex : min(p_col, k_ex));    // first ':' (in the tile) of the open line
+        ofc = (int)(c_ex ? k_ex : min(p_col, k_ex));    // first ':' (in the tile) of the open line
     };
-    const uint32_t l_in = wave_incl_max32(nlm ? (uint32_t)tid + 1u : 0u);
-    const uint32_t k_in = wave_incl_min32(((uint32_t)(BLOCK - (int)l_in) << 17) | lane_cand(nlm, clm));
+    const uint32_t k_in = wave_incl_min32(((8191u - c_in) << 17) | lane_cand(nlm, clm));
     // one '\n' at most in every chunk of the wave (the one-line-per-lane path below)
     const uint32_t multi = __ballot(__popcll(nlm) > 1) != 0ull ? 1u : 0u;
-    if (lane == 63) *(uint4 *)&sm.wave_scan[wave][0] = make_uint4(c_in, l_in, k_in, multi);
+    if (lane == 63) *(uint4 *)&sm.wave_scan[wave][0] = make_uint4(c_in, 0u, k_in, multi);
     wg_barrier();
     stamp<ABL>(p, tid, g, 2);
     int lane_first, open_fc;
-    lane_state(c_in, l_in, k_in, lane_first, open_fc);
+    lane_state(c_in, k_in, lane_first, open_fc);
     uint32_t multi_any = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) multi_any |= sm.wave_scan[w][3];
@@ -1616,10 +1615,9 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
             const uint64_t cl = ((uint64_t)__builtin_amdgcn_perm(m[3], m[2], 0x07060302u) << 32) |
                                 __builtin_amdgcn_perm(m[1], m[0], 0x07060302u);
             const uint32_t cin = wave_incl_add32((uint32_t)__popcll(nl));
-            const uint32_t lin = wave_incl_max32(nl ? (uint32_t)tid + 1u : 0u);
-            const uint32_t kin = wave_incl_min32(((uint32_t)(BLOCK - (int)lin) << 17) | lane_cand(nl, cl));
+            const uint32_t kin = wave_incl_min32(((8191u - cin) << 17) | lane_cand(nl, cl));
             int lf, ofc;
-            lane_state(cin, lin, kin, lf, ofc);
+            lane_state(cin, kin, lf, ofc);
             stage(wbase, nl, cl, lf, ofc);
         }
     }
