@@ -1227,7 +1227,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
     } else {
     // ---- per lane: '\n' / ':' masks of its 64 contiguous bytes, segmented line-state scan -------
     const int o = tid * kLaneBytes;   // tile position of the lane's first byte (nlm / clm bit i: byte o + i)
-    // Line state before each lane's chunk, by three u32 wave scans (DPP) and a prefix over the
+    // Line state before each lane's chunk, by two u32 wave scans (DPP) and a prefix over the
     // earlier waves: the number of '\n' before it, and the first ':' of the line open at its start.
     //  * the colon candidate of a chunk is its first ':' after its last '\n' (or its first ':' if it
     //    holds no '\n'): the first ':' of the line open at a chunk's end is the smallest candidate
