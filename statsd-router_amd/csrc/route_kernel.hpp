@@ -369,6 +369,7 @@ __device__ __forceinline__ uint64_t div_magic(uint64_t n, const Magic &mg) {
 }
 
 __device__ __forceinline__ uint32_t mod_magic(uint64_t n, const Magic &mg, uint32_t d) {
+    if (mg.kind == 0) return (uint32_t)n & (d - 1u);   // d a power of two (make_magic)
     return (uint32_t)(n - div_magic(n, mg) * (uint64_t)d);
 }
 
