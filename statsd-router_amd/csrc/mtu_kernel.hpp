@@ -39,9 +39,9 @@
 namespace srk {
 
 constexpr int kMtuTile = 512;                    // records per sort tile (one wave)
-constexpr int kMtuChunk = 4096;                  // sorted lines per packing chunk
+constexpr int kMtuChunk = 4096;                  // sorted lines per packing chunk (the larger size)
+constexpr int kMtuChunkSmall = 2048;             // ... the smaller: twice the chunks in flight, twice the chain
 constexpr int kMtuBlock = 256;                   // threads of the chunk kernels
-constexpr int kMtuPer = kMtuChunk / kMtuBlock;   // lines per thread in a chunk
 constexpr uint32_t kMtuMaxShards = 4096;
 constexpr int kMtuCap = (int)SR_DOWNSTREAM_BUF_SIZE;   // 1450: sr-types.h:30
 constexpr int kMtuWindow = kMtuCap / (int)SR_MIN_LINE_LENGTH + 1;   // a packet holds < 242 lines
@@ -77,6 +77,7 @@ struct MtuBatchArg {
 
 struct MtuLaunch {
     uint32_t nds, nb, tiles, chunks;   // shards; batches; record tiles and chunks of all batches
+    uint32_t chunk_lines;              // lines per chunk of this launch (kMtuChunk or kMtuChunkSmall)
     uint32_t *tile_counts;             // batch b at (nds + 1) * tile0: [(nds + 1) * ntiles], key-major
     uint32_t *keys;                    // [nb][2 * nds + 4]: key starts (nds + 2) | chunk firsts (nds + 1)
     uint32_t *chunk_shard;             // [chunks]
@@ -99,6 +100,7 @@ struct MtuParams {
     uint32_t nds;             // shards; key nds = unrouted lines
     uint32_t ntiles;          // record tiles of the batch
     uint32_t max_chunks;      // chunks of the batch
+    uint32_t chunk_lines;     // lines per chunk
     const uint16_t *fill_in;
     const uint64_t *probed_dead;
     uint32_t *tile_counts;    // [(nds + 1) * ntiles], key-major; scanned in place
@@ -127,6 +129,7 @@ __device__ __forceinline__ MtuParams mtu_view(const MtuLaunch &L, uint32_t bi) {
     p.nds = L.nds;
     p.ntiles = (bi + 1 < L.nb ? L.b[bi + 1].tile0 : L.tiles) - a.tile0;
     p.max_chunks = (bi + 1 < L.nb ? L.b[bi + 1].chunk0 : L.chunks) - a.chunk0;
+    p.chunk_lines = L.chunk_lines;
     p.fill_in = a.fill_in;
     p.probed_dead = a.probed_dead;
     p.tile_counts = L.tile_counts + (size_t)(L.nds + 1) * a.tile0;
@@ -268,7 +271,7 @@ __global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuLaunch L) {
     uint32_t loc = 0;
     for (uint32_t s = tid * per; s < (tid + 1) * per && s < p.nds; ++s) {
         const uint32_t c = p.key_start[s + 1] - p.key_start[s];
-        loc += (c + kMtuChunk - 1) / kMtuChunk;
+        loc += (c + p.chunk_lines - 1) / p.chunk_lines;
     }
     const uint32_t incl = wave_incl_add32(loc);
     if (lane == 63) wsum[wave] = incl;
@@ -278,7 +281,7 @@ __global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuLaunch L) {
     for (uint32_t s = tid * per; s < (tid + 1) * per && s < p.nds; ++s) {
         p.chunk_first[s] = run;
         const uint32_t c = p.key_start[s + 1] - p.key_start[s];
-        const uint32_t nc = (c + kMtuChunk - 1) / kMtuChunk;
+        const uint32_t nc = (c + p.chunk_lines - 1) / p.chunk_lines;
         for (uint32_t j = 0; j < nc; ++j)
             if (run + j < p.max_chunks) p.chunk_shard[run + j] = s;
         run += nc;
@@ -336,18 +339,21 @@ __global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_scatter_kernel(MtuLaun
 }
 
 // ---- packing: per-chunk next-fit tables -------------------------------------------------------
-// LDS of the two chunk kernels, kept apart so that each holds only what it reads (32 KiB: five
-// workgroups per CU instead of three; 20 KiB for emit). The prefix scan's wave sums borrow ld / nx.
+// LDS of the two chunk kernels, kept apart so that each holds only what it reads (4096-line chunks:
+// 32 KiB, five workgroups per CU instead of three; 20 KiB for emit; half that for 2048-line chunks).
+// The prefix scan's wave sums borrow ld / nx.
+template <int CH>
 struct MtuTableSmem {
-    uint32_t P[kMtuChunk];      // inclusive prefix of the chunk's line lengths
-    uint32_t ld[kMtuChunk];     // last packet start reached from here << 16 | packets closed on the way
+    uint32_t P[CH];      // inclusive prefix of the chunk's line lengths
+    uint32_t ld[CH];     // last packet start reached from here << 16 | packets closed on the way
 };
 constexpr int kMtuHop = 16;   // packets per anchor of the emit walk
+template <int CH>
 struct MtuEmitSmem {
-    uint32_t P[kMtuChunk];
-    alignas(16) uint8_t nx[kMtuChunk];   // next(i) - i (1 .. kMtuWindow - 1), 0 = none in the chunk
-    uint16_t J[kMtuChunk];               // kMtuHop packet starts ahead on the chain (kMtuEnd: it ends first)
-    uint16_t anchor[kMtuChunk / kMtuHop + 2];
+    uint32_t P[CH];
+    alignas(16) uint8_t nx[CH];   // next(i) - i (1 .. kMtuWindow - 1), 0 = none in the chunk
+    uint16_t J[CH];               // kMtuHop packet starts ahead on the chain (kMtuEnd: it ends first)
+    uint16_t anchor[CH / kMtuHop + 2];
     uint32_t nanchor;
 };
 
@@ -360,8 +366,8 @@ __device__ __forceinline__ bool mtu_chunk_of(const MtuParams &p, uint32_t c, Mtu
     if (c >= min(p.chunk_first[p.nds], p.max_chunks)) return false;
     ck.shard = p.chunk_shard[c];
     const uint32_t s0 = p.key_start[ck.shard], s1 = p.key_start[ck.shard + 1];
-    ck.pos0 = s0 + (c - p.chunk_first[ck.shard]) * kMtuChunk;
-    ck.cnt = min((uint32_t)kMtuChunk, s1 - ck.pos0);
+    ck.pos0 = s0 + (c - p.chunk_first[ck.shard]) * p.chunk_lines;
+    ck.cnt = min(p.chunk_lines, s1 - ck.pos0);
     ck.last = ck.pos0 + ck.cnt == s1;
     return true;
 }
@@ -379,15 +385,17 @@ __device__ __forceinline__ uint32_t mtu_first_over(const uint32_t *P, uint32_t l
 // LDS prefix sums of the chunk's lengths. Wave w owns lines [1024 w, 1024 w + 1024), lane-
 // interleaved (line 1024 w + 64 k + lane): coalesced record loads, conflict-free LDS stores, the
 // running sum carried across the wave's 16 rows by DPP scans; one barrier for the wave offsets.
+template <int CH>
 __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuChunk &ck, uint32_t *P,
                                                  uint32_t *wsum) {
+    constexpr int kMtuPer = CH / kMtuBlock;
     if (SR_MTU_SKIP & 16) {
-        for (uint32_t i = threadIdx.x; i < (uint32_t)kMtuChunk; i += kMtuBlock) P[i] = 64u * (i + 1);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)CH; i += kMtuBlock) P[i] = 64u * (i + 1);
         __syncthreads();
         return;
     }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t base = (uint32_t)wave * (kMtuChunk / (kMtuBlock / 64)) + (uint32_t)lane;
+    const uint32_t base = (uint32_t)wave * (CH / (kMtuBlock / 64)) + (uint32_t)lane;
     uint32_t v[kMtuPer];
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) {   // unconditional (clamped) loads: all 16 in flight together
@@ -414,8 +422,9 @@ __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuCh
 // chunk), for lines tid + 256 k: a fixed 8-step search over the 256 lines after i (a packet holds
 // fewer than 242), the 16 searches of a thread independent, neighbouring lanes on neighbouring
 // words. f(i, next) stores the result.
-template <typename F>
+template <int CH, typename F>
 __device__ __forceinline__ void mtu_chunk_next(const uint32_t *P, uint32_t cnt, F f) {
+    constexpr int kMtuPer = CH / kMtuBlock;
     if (SR_MTU_SKIP & 8) {
         for (uint32_t i = threadIdx.x; i < cnt; i += kMtuBlock) f(i, i + 22 < cnt ? (uint16_t)(i + 22) : kMtuEnd);
         return;
@@ -450,8 +459,10 @@ __device__ __forceinline__ void mtu_chunk_next(const uint32_t *P, uint32_t cnt, 
 }
 
 // table[c][x] = (packets closed << 32) | (last packet start << 16, 0xFFFF = none) | fill after
+template <int CH>
 __global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
-    __shared__ MtuTableSmem sm;
+    constexpr int kMtuPer = CH / kMtuBlock;
+    __shared__ MtuTableSmem<CH> sm;
     MtuChunk ck;
     const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.chunk0; });
     const MtuParams p = mtu_view(L, bi);
@@ -459,14 +470,14 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
     if (!mtu_chunk_of(p, c, ck)) return;
     const int tid = threadIdx.x;
     mtu_stamp(L, blockIdx.x, 0);
-    mtu_chunk_prefix(p, ck, sm.P, sm.ld);
+    mtu_chunk_prefix<CH>(p, ck, sm.P, sm.ld);
     mtu_stamp(L, blockIdx.x, 1);
     uint8_t *gnx = p.nx + (size_t)c * kMtuChunk;
-    mtu_chunk_next(sm.P, ck.cnt, [&](uint32_t i, uint16_t nxt) {
+    mtu_chunk_next<CH>(sm.P, ck.cnt, [&](uint32_t i, uint16_t nxt) {
         sm.ld[i] = nxt == kMtuEnd ? i << 16 : ((uint32_t)nxt << 16) | 1u;
         if (!(SR_MTU_SKIP & 32)) gnx[i] = nxt == kMtuEnd ? 0 : (uint8_t)(nxt - i);   // for mtu_emit
     });
-    for (uint32_t i = ck.cnt + (uint32_t)tid; i < (uint32_t)kMtuChunk; i += kMtuBlock) sm.ld[i] = i << 16;   // self loops
+    for (uint32_t i = ck.cnt + (uint32_t)tid; i < (uint32_t)CH; i += kMtuBlock) sm.ld[i] = i << 16;   // self loops
     __syncthreads();
     mtu_stamp(L, blockIdx.x, 2);
     const uint32_t total = sm.P[ck.cnt - 1];
@@ -534,7 +545,7 @@ __global__ __launch_bounds__(1024) void mtu_chain_kernel(MtuLaunch L) {
             const uint32_t cl = (uint32_t)(e >> 32);
             if (cl) {
                 closed += cl;
-                open = p.key_start[s] + (c - c0) * kMtuChunk + (uint32_t)((e >> 16) & 0xFFFFu);
+                open = p.key_start[s] + (c - c0) * p.chunk_lines + (uint32_t)((e >> 16) & 0xFFFFu);
             }
             x = (uint32_t)(e & 0xFFFFu);
         }
@@ -573,8 +584,10 @@ __device__ __forceinline__ void mtu_put(const MtuParams &p, uint32_t k, uint32_t
 // four rounds of pointer doubling give every line the start kMtuHop packets ahead (J); one thread
 // walks the chain by those hops, leaving an anchor every kMtuHop packets; then every anchor's
 // thread walks its kMtuHop packets by next() and writes their descriptors (rank = 16 q + step).
+template <int CH>
 __global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuLaunch L) {
-    __shared__ MtuEmitSmem sm;
+    constexpr int kMtuPer = CH / kMtuBlock;
+    __shared__ MtuEmitSmem<CH> sm;
     MtuChunk ck;
     const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.chunk0; });
     const MtuParams p = mtu_view(L, bi);
@@ -585,8 +598,8 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuLaunch L) {
     {   // next(i) - i as mtu_table stored it: 16 bytes per thread
         const uint4 *src = reinterpret_cast<const uint4 *>(p.nx + (size_t)c * kMtuChunk);
         const uint4 v = (uint32_t)tid * 16 < ck.cnt ? src[tid] : make_uint4(0, 0, 0, 0);
-        mtu_chunk_prefix(p, ck, sm.P, reinterpret_cast<uint32_t *>(sm.J));
-        reinterpret_cast<uint4 *>(sm.nx)[tid] = v;
+        mtu_chunk_prefix<CH>(p, ck, sm.P, reinterpret_cast<uint32_t *>(sm.J));
+        if ((uint32_t)tid * 16 < (uint32_t)CH) reinterpret_cast<uint4 *>(sm.nx)[tid] = v;
     }
     __syncthreads();
     mtu_stamp(L, blockIdx.x, 6);

@@ -364,6 +364,13 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     if (nds > SR_MAX_PACK_DOWNSTREAMS) return -EINVAL;
     MtuLaunch L;
     memset(&L, 0, sizeof(L));
+    // Chunk size: a shard's chunks are composed one after another (mtu_chain), so few shards with
+    // many lines each want long chunks; many shards (short chains) want more, smaller chunks in
+    // flight (2048 lines: 16 KiB of LDS per table workgroup, ten per CU instead of five).
+    uint64_t all_records = 0;
+    for (size_t j = 0; j < count; ++j) all_records += batches[j].max_records;
+    const uint32_t ch = all_records <= (uint64_t)(nds ? nds : 1) * 32u * kMtuChunk ? (uint32_t)kMtuChunkSmall
+                                                                                  : (uint32_t)kMtuChunk;
     uint32_t tiles = 0, chunks = 0;
     for (size_t j = 0; j < count; ++j) {
         const sr_pack_batch &b = batches[j];
@@ -385,7 +392,7 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
         a.chunk0 = chunks;
         const uint64_t nt = (b.max_records + kMtuTile - 1) / kMtuTile;
         tiles += (uint32_t)(nt ? nt : 1);
-        chunks += (uint32_t)((b.max_records + kMtuChunk - 1) / kMtuChunk) + nds + 1;
+        chunks += (uint32_t)((b.max_records + ch - 1) / ch) + nds + 1;
     }
     (void)hipSetDevice(c->device);
     int rc = mtu_reserve(c, tiles, chunks, (uint32_t)count);
@@ -394,6 +401,7 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     L.nb = (uint32_t)count;
     L.tiles = tiles;
     L.chunks = chunks;
+    L.chunk_lines = ch;
     L.tile_counts = c->d_mtu_tiles;
     L.keys = c->d_mtu_keys;
     L.closed = c->d_mtu_keys + (size_t)kMtuMaxBatches * (2 * (size_t)nds + 4);
@@ -431,9 +439,15 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     hipLaunchKernelGGL(mtu_count_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
     hipLaunchKernelGGL(mtu_scan_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
     hipLaunchKernelGGL(mtu_scatter_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
-    hipLaunchKernelGGL(mtu_table_kernel, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
+    if (ch == (uint32_t)kMtuChunk)
+        hipLaunchKernelGGL(mtu_table_kernel<kMtuChunk>, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
+    else
+        hipLaunchKernelGGL(mtu_table_kernel<kMtuChunkSmall>, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
     hipLaunchKernelGGL(mtu_chain_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
-    hipLaunchKernelGGL(mtu_emit_kernel, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
+    if (ch == (uint32_t)kMtuChunk)
+        hipLaunchKernelGGL(mtu_emit_kernel<kMtuChunk>, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
+    else
+        hipLaunchKernelGGL(mtu_emit_kernel<kMtuChunkSmall>, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 

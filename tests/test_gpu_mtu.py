@@ -33,6 +33,8 @@ STREAMS = [
     ([64], 1, 0.0, 0.0, 1 << 18, 9),
     ([64, 256], 300, 0.3, 0.1, 1 << 19, 10),
     ([64], 4, 1.0, 0.0, 1 << 16, 11),              # every downstream dead
+    ([6, 7], 1, 0.0, 0.0, 1 << 20, 12),            # one shard, > 131 k line capacity: 4096-line chunks
+    ([6, 7], 2, 0.5, 0.0, 1 << 20, 13),            # the same through the probe, one shard alive
 ]
 
 
