@@ -35,6 +35,7 @@ import platform
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
@@ -72,6 +73,8 @@ def parse(argv=None):
     ap.add_argument("--regroup-config", default="c5", choices=sorted(CONFIGS))
     ap.add_argument("--regroup-steps", type=int, default=8)
     ap.add_argument("--regroup-batches", type=int, default=32, help="batches per regroup step (one route launch)")
+    ap.add_argument("--regroup-timeout", type=float, default=240.0,
+                    help="seconds the regroup leg may take before every rank gives it up (the main line is still printed)")
     ap.add_argument("--exchange", default="c", choices=["c", "torch"],
                     help="regroup transport: the C ABI's RCCL exchange or torch.distributed")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
@@ -322,7 +325,29 @@ def main(argv=None):
     router.close()
     del d_in, d_out
     torch.cuda.empty_cache()
+    emitted = threading.Lock()   # held by whoever prints the line (once)
+
+    def emit(res):
+        if emitted.acquire(blocking=False):
+            if rank == 0:
+                print(json.dumps(res), file=json_out, flush=True)
+            return True
+        return False
+
+    dog = None
     if args.regroup == "on" or (args.regroup == "auto" and world > 1):
+        # a collective that never completes (a peer lost, a transport stuck) must not take the main
+        # line with it: past the deadline every rank prints what it has and leaves
+        def give_up():
+            if rank == 0:
+                result["regroup"] = {"error": f"timed out after {args.regroup_timeout:.0f} s"}
+            emit(result)
+            sys.stderr.flush()
+            os._exit(0)
+
+        dog = threading.Timer(args.regroup_timeout, give_up)
+        dog.daemon = True
+        dog.start()
         try:   # a failing regroup leg must not take the main line with it
             rg = regroup_leg(pkg, dev, local, world, rank, args.regroup_config, args.regroup_steps,
                              per_step=args.regroup_batches, exchange=args.exchange)
@@ -330,10 +355,11 @@ def main(argv=None):
             rg = {"error": f"{type(e).__name__}: {e}"}
         if rank == 0:
             result["regroup"] = rg
-    if rank == 0:
-        print(json.dumps(result), file=json_out, flush=True)
+    emit(result)
     if dist.is_initialized():
         dist.destroy_process_group()
+    if dog is not None:
+        dog.cancel()
 
 
 def read_ceiling(d_in, stream, reps=20):
