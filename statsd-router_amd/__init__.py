@@ -447,8 +447,15 @@ class Comm:
     def from_group(cls, device: int, group=None) -> "Comm":
         """Every rank of a torch.distributed group joins one communicator (rank 0 makes the id)."""
         import torch.distributed as dist
-        box = [cls.new_id() if dist.get_rank(group) == 0 else None]
+        box = [None]
+        if dist.get_rank(group) == 0:   # a failure here still reaches every rank (no rank left waiting)
+            try:
+                box[0] = cls.new_id()
+            except (OSError, RuntimeError) as e:
+                box[0] = f"{type(e).__name__}: {e}"
         dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        if isinstance(box[0], str):
+            raise RuntimeError(f"rank 0 could not make the communicator id: {box[0]}")
         return cls(box[0], dist.get_world_size(group), dist.get_rank(group), device)
 
     def close(self) -> None:

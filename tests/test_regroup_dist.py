@@ -122,3 +122,64 @@ def test_pack_oracle_layout(pkg, oracle):
             pos += int(x["length"]) + pad
         assert pos == cnt[o, 1]
     assert k == len(pr) == int(cnt[:, 0].sum())
+
+
+def _comm_worker(rank, world, port, fail, q):
+    """Comm.from_group over gloo with the C ABI calls replaced: every rank must see rank 0's id, and a
+    failure to make the id on rank 0 must reach every rank as an error (no rank left waiting)."""
+    try:
+        sys.path.insert(0, REPO)
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pkg = importlib.import_module("statsd-router_amd")
+        seen = {}
+
+        def new_id():
+            if fail:
+                raise pkg.SrError(5, "sr_comm_id: Input/output error")
+            return bytes([rank + 1]) * pkg.SR_COMM_ID_BYTES
+
+        def init(self, comm_id, w, r, device):
+            seen.update(id=comm_id, world=w, rank=r, device=device)
+
+        pkg.Comm.new_id = staticmethod(new_id)
+        pkg.Comm.__init__ = init
+        try:
+            pkg.Comm.from_group(device=3)
+            out = seen
+        except RuntimeError as e:
+            out = {"error": str(e)}
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, out))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("fail", [False, True])
+def test_comm_from_group_gloo(fail):
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, fail, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            rank, out = q.get(timeout=240)
+            res[rank] = out
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert isinstance(res[r], dict), res[r]
+        if fail:
+            assert "sr_comm_id" in res[r]["error"]
+        else:
+            assert res[r] == {"id": b"\x01" * 128, "world": world, "rank": r, "device": 3}
