@@ -1553,7 +1553,11 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     const uint32_t k = x >> 6;   // the lane word: wave-uniform
                     const bool act = x < TL;
                     // a wave without a segment in this round only meets the barrier
-                    const bool live = r0 + wave * 64 < (int)TL;
+                    const bool live = r0 + wave * 64 < (int)TL
+#ifdef SR_SEG_ONE_ROUND   // timing bound only (wrong records): no segment work past a tile's first round
+                                      && r0 == 0
+#endif
+                        ;
                     uint64_t below = 0, part = 0;
                     int sg = 0, glast = -1, j = 0, s = 0, len = 0;
                     bool len_ok = false, fmt_ok = false;
