@@ -215,6 +215,53 @@ int sr_exchange_data(sr_ctx *ctx, sr_comm *comm, const uint8_t *d_packed, const 
                      const uint64_t *h_sent, const uint64_t *h_received, uint8_t *d_recv_bytes,
                      sr_record *d_recv_recs);
 
+/* The plan of one exchange (host only, no GPU): what sr_exchange_data moves to and from each peer.
+ * For peer q, the pack's records [send_line0, send_line0 + send_lines) and bytes [send_byte0, +send_bytes)
+ * go to q; q's chunk lands at records [recv_line0, +recv_lines) and bytes [recv_byte0, +recv_bytes) of
+ * the receive buffers, and its records' offsets move by recv_byte0 (the rebase). peers[rank] is the
+ * rank's own chunk: a local copy, not a send. The reference analogue is the SO_REUSEPORT split of
+ * datagrams over data threads (sr-main.c:253-271,363-367); the plan is what regroups them by owner. */
+typedef struct sr_exchange_peer {
+    uint64_t send_line0, send_lines, send_byte0, send_bytes;
+    uint64_t recv_line0, recv_lines, recv_byte0, recv_bytes;
+} sr_exchange_peer;
+
+/* Fill peers[world] from the split sizes (u64 [world][2] {lines, bytes}, as sr_exchange_sizes returns
+ * them) and totals[4] = {lines sent, bytes sent, lines received, bytes received} (totals may be NULL).
+ * Returns 0, or -EINVAL: bad world/rank, the own chunk's sent and received sizes differ, or a received
+ * total does not fit the u32 record offsets. */
+int sr_exchange_plan(int world, int rank, const uint64_t *h_sent, const uint64_t *h_received,
+                     sr_exchange_peer *peers, uint64_t *totals);
+
+/* The transport an exchange runs on. sr_exchange_data uses RCCL (ncclSend/ncclRecv in one group, the
+ * own chunk by hipMemcpyAsync, the rebase by a kernel, all on the context's stream); a host that moves
+ * the chunks another way (tests: torch.distributed gloo over host memory) supplies its own. Every
+ * callback returns 0 or a negative errno. tag 0 = line bytes, 1 = records (a send of `bytes` bytes to
+ * `peer` matches that peer's recv of the same tag from this rank). rebase: add peers[p].recv_byte0 to
+ * the offset of records [recv_line0, +recv_lines) of every source p. */
+typedef struct sr_transport {
+    void *user;
+    int (*group_start)(void *user);
+    int (*group_end)(void *user);
+    int (*send)(void *user, const void *buf, size_t bytes, int peer, int tag);
+    int (*recv)(void *user, void *buf, size_t bytes, int peer, int tag);
+    int (*copy)(void *user, void *dst, const void *src, size_t bytes);
+    int (*rebase)(void *user, sr_record *recs, const sr_exchange_peer *peers, int world, uint64_t n_lines);
+} sr_transport;
+
+/* One exchange on a caller-supplied transport: sr_exchange_plan, then within one group_start/group_end
+ * the sends and receives of every peer q != rank in rank order (bytes, then records; zero-sized ones
+ * skipped), then the own chunk's copies, then one rebase of all received records. Buffers are whatever
+ * the transport addresses (device memory for RCCL). Returns 0, -EINVAL or the first callback error. */
+int sr_exchange_run(const sr_transport *t, int world, int rank, const uint64_t *h_sent,
+                    const uint64_t *h_received, const uint8_t *packed, const sr_record *packed_recs,
+                    uint8_t *recv_bytes, sr_record *recv_recs);
+
+/* The rebase of sr_exchange_data alone (asynchronous on the context's stream): records
+ * [peers[p].recv_line0, +recv_lines) of d_recv_recs move by peers[p].recv_byte0, p = 0..world-1.
+ * world <= SR_MAX_OWNERS; the sources' record ranges must be back to back from 0. Returns 0, -EINVAL, -EIO. */
+int sr_exchange_rebase(sr_ctx *ctx, sr_record *d_recv_recs, const sr_exchange_peer *peers, int world);
+
 /* ---- per-downstream MTU packing ------------------------------------------ */
 /* push_to_downstream (sr-main.c:73-83) appends each routed line to its downstream's active buffer,
  * flushing the buffer first when the line would not fit in DOWNSTREAM_BUF_SIZE (1450) bytes

@@ -51,6 +51,7 @@ ABI_FUNCTIONS = (
     "sr_route_batch", "sr_last_probed_dead", "sr_route_device", "sr_route_device_many", "sr_pack_by_owner",
     "sr_pack_many_by_owner", "sr_pack_packets", "sr_pack_packets_many", "sr_route_pack_batch", "sr_alloc_host", "sr_free_host", "sr_sync", "sr_close", "sr_version",
     "sr_comm_id", "sr_comm_open", "sr_comm_close", "sr_exchange_sizes", "sr_exchange_data",
+    "sr_exchange_plan", "sr_exchange_run", "sr_exchange_rebase",
 )
 SR_MAX_PACK_DOWNSTREAMS = 4096
 SR_LAYOUT_AUTO, SR_LAYOUT_UNIFORM, SR_LAYOUT_SEGMENTS = 0, 1, 2
@@ -90,6 +91,28 @@ class SrPackBatch(ctypes.Structure):
         ("d_packets", ctypes.c_void_p), ("max_packets", ctypes.c_size_t), ("d_counts", ctypes.c_void_p),
         ("d_fill_out", ctypes.c_void_p),
     ]
+
+
+class SrExchangePeer(ctypes.Structure):
+    """struct sr_exchange_peer (include/sr_route.h): one peer's share of an exchange plan."""
+    _fields_ = [(n, ctypes.c_uint64) for n in ("send_line0", "send_lines", "send_byte0", "send_bytes",
+                                               "recv_line0", "recv_lines", "recv_byte0", "recv_bytes")]
+
+
+PEER_DTYPE = np.dtype([(n, "<u8") for n, _ in SrExchangePeer._fields_])
+
+_GROUP_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+_SEND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int,
+                            ctypes.c_int)
+_COPY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+_REBASE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(SrExchangePeer),
+                              ctypes.c_int, ctypes.c_uint64)
+
+
+class SrTransport(ctypes.Structure):
+    """struct sr_transport (include/sr_route.h)."""
+    _fields_ = [("user", ctypes.c_void_p), ("group_start", _GROUP_FN), ("group_end", _GROUP_FN),
+                ("send", _SEND_FN), ("recv", _SEND_FN), ("copy", _COPY_FN), ("rebase", _REBASE_FN)]
 
 
 class SrError(OSError):
@@ -158,6 +181,10 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_comm_close": (None, [vp]),
         "sr_exchange_sizes": (ctypes.c_int, [vp, vp, vp, vp, vp, vp]),
         "sr_exchange_data": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp]),
+        "sr_exchange_plan": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, vp, vp, vp, vp]),
+        "sr_exchange_run": (ctypes.c_int, [ctypes.POINTER(SrTransport), ctypes.c_int, ctypes.c_int, vp, vp, vp, vp,
+                                           vp, vp]),
+        "sr_exchange_rebase": (ctypes.c_int, [vp, vp, vp, ctypes.c_int]),
     }
     for name in ABI_FUNCTIONS:
         fn = getattr(lib, name)  # raises AttributeError if the export is missing
@@ -421,6 +448,12 @@ class Router:
                                           received.ctypes.data, vp(d_recv_bytes), vp(d_recv_recs)),
                "sr_exchange_data")
 
+    def exchange_rebase(self, d_recv_recs: int, peers: np.ndarray) -> None:
+        """sr_exchange_rebase: the exchange's record rebase alone (asynchronous on the router's stream)."""
+        p = np.ascontiguousarray(peers, dtype=PEER_DTYPE)
+        _check(self._lib.sr_exchange_rebase(self._h, ctypes.c_void_p(d_recv_recs), p.ctypes.data, int(p.size)),
+               "sr_exchange_rebase")
+
     def sync(self) -> None:
         _check(self._lib.sr_sync(self._h), "sr_sync")
 
@@ -462,6 +495,92 @@ class Comm:
         if self.handle:
             self._lib.sr_comm_close(self.handle)
             self.handle = ctypes.c_void_p()
+
+
+def exchange_plan(world: int, rank: int, sent, received):
+    """sr_exchange_plan (host only): returns (peers: PEER_DTYPE [world], totals: u64 [4] = {lines sent,
+    bytes sent, lines received, bytes received})."""
+    s = np.ascontiguousarray(sent, dtype=np.uint64).reshape(-1)
+    r = np.ascontiguousarray(received, dtype=np.uint64).reshape(-1)
+    if s.size != 2 * world or r.size != 2 * world:
+        raise ValueError("split sizes must be [world, 2]")
+    peers = np.zeros(max(world, 1), dtype=PEER_DTYPE)
+    tot = np.zeros(4, dtype=np.uint64)
+    _check(lib().sr_exchange_plan(world, rank, s.ctypes.data, r.ctypes.data, peers.ctypes.data, tot.ctypes.data),
+           "sr_exchange_plan")
+    return peers, tot
+
+
+class Transport:
+    """A transport for sr_exchange_run written in Python (override the methods; raise to fail).
+    Addresses are plain integers; what they address (host or device memory) is the transport's business."""
+
+    def group_start(self) -> None:
+        pass
+
+    def group_end(self) -> None:
+        pass
+
+    def send(self, addr: int, nbytes: int, peer: int, tag: int) -> None:
+        raise NotImplementedError
+
+    def recv(self, addr: int, nbytes: int, peer: int, tag: int) -> None:
+        raise NotImplementedError
+
+    def copy(self, dst: int, src: int, nbytes: int) -> None:
+        ctypes.memmove(dst, src, nbytes)
+
+    def rebase(self, recs_addr: int, peers: np.ndarray, n_lines: int) -> None:
+        """Host memory: records [recv_line0, +recv_lines) of every source move by its recv_byte0."""
+        recs = host_records(recs_addr, n_lines)
+        for p in peers:
+            a, n = int(p["recv_line0"]), int(p["recv_lines"])
+            recs["offset"][a: a + n] += np.uint32(p["recv_byte0"])
+
+
+def host_records(addr: int, n: int) -> np.ndarray:
+    """A writable RECORD_DTYPE view of n records at a host address."""
+    if n == 0:
+        return np.zeros(0, dtype=RECORD_DTYPE)
+    return np.frombuffer((ctypes.c_uint8 * (8 * n)).from_address(addr), dtype=RECORD_DTYPE)
+
+
+def exchange_run(transport: Transport, world: int, rank: int, sent, received, packed: int, packed_recs: int,
+                 recv_bytes: int, recv_recs: int) -> None:
+    """sr_exchange_run: the C exchange plan and its calls, on a Python transport."""
+    err = []
+
+    def wrap(fn):
+        def call(*a):
+            try:
+                fn(*a)
+                return 0
+            except Exception as e:   # noqa: BLE001 - reported after the C call returns
+                err.append(e)
+                return -errno.EIO
+        return call
+
+    def rebase(_u, recs, peers_p, w, n):
+        arr = np.ctypeslib.as_array(ctypes.cast(peers_p, ctypes.POINTER(ctypes.c_uint64)), shape=(w * 8,))
+        transport.rebase(recs, arr.copy().view(PEER_DTYPE), int(n))
+
+    cb = SrTransport(None,
+                     _GROUP_FN(wrap(lambda _u: transport.group_start())),
+                     _GROUP_FN(wrap(lambda _u: transport.group_end())),
+                     _SEND_FN(wrap(lambda _u, b, n, p, t: transport.send(b, n, p, t))),
+                     _SEND_FN(wrap(lambda _u, b, n, p, t: transport.recv(b, n, p, t))),
+                     _COPY_FN(wrap(lambda _u, d, s, n: transport.copy(d, s, n))),
+                     _REBASE_FN(wrap(rebase)))
+    s = np.ascontiguousarray(sent, dtype=np.uint64).reshape(-1)
+    r = np.ascontiguousarray(received, dtype=np.uint64).reshape(-1)
+    if s.size != 2 * world or r.size != 2 * world:
+        raise ValueError("split sizes must be [world, 2]")
+    vp = ctypes.c_void_p
+    rc = lib().sr_exchange_run(ctypes.byref(cb), world, rank, s.ctypes.data, r.ctypes.data, vp(packed),
+                               vp(packed_recs), vp(recv_bytes), vp(recv_recs))
+    if err:
+        raise err[0]
+    _check(rc, "sr_exchange_run")
 
 
 def version() -> str:

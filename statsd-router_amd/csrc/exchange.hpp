@@ -15,9 +15,12 @@
 #pragma once
 
 #include <dlfcn.h>
+#include <errno.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
+
+#include <mutex>
 
 #include "regroup_kernel.hpp"
 
@@ -42,11 +45,7 @@ struct CommId {
 };
 using InitRankFn = int (*)(void **, int, CommId, int);
 
-inline RcclApi *rccl_api() {
-    static RcclApi api;
-    static bool tried = false;
-    if (tried) return api.so ? &api : nullptr;
-    tried = true;
+inline RcclApi *rccl_load(RcclApi &api) {
     void *so = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);   // already in the process
     if (!so) so = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
     if (!so) so = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
@@ -66,6 +65,14 @@ inline RcclApi *rccl_api() {
     return &api;
 }
 
+inline RcclApi *rccl_api() {   // loaded once per process (data threads may race here)
+    static RcclApi api;
+    static RcclApi *loaded = nullptr;
+    static std::once_flag once;
+    std::call_once(once, [] { loaded = rccl_load(api); });
+    return loaded;
+}
+
 // Received records from source p (lines [line0[p], line0[p+1])) move by byte0[p].
 struct RebaseArgs {
     uint32_t sources;
@@ -73,6 +80,85 @@ struct RebaseArgs {
     uint32_t line0[kMaxOwners + 1];
     uint32_t byte0[kMaxOwners];
 };
+
+// The exchange plan (sr_exchange_plan): per peer the pack's chunk sent to it and where its chunk
+// lands. Chunks are owner-major in the pack (sr_pack_many_by_owner) and source-major in the receive
+// buffers, so both sides are exclusive prefix sums of the split sizes.
+inline int exchange_plan(int world, int rank, const uint64_t *sent, const uint64_t *received,
+                         sr_exchange_peer *peers, uint64_t totals[4]) {
+    if (world < 1 || world > kMaxOwners || rank < 0 || rank >= world || !sent || !received || !peers)
+        return -EINVAL;
+    uint64_t s_l = 0, s_b = 0, r_l = 0, r_b = 0;
+    for (int q = 0; q < world; ++q) {
+        sr_exchange_peer &e = peers[q];
+        e.send_line0 = s_l, e.send_lines = sent[2 * q];
+        e.send_byte0 = s_b, e.send_bytes = sent[2 * q + 1];
+        e.recv_line0 = r_l, e.recv_lines = received[2 * q];
+        e.recv_byte0 = r_b, e.recv_bytes = received[2 * q + 1];
+        s_l += e.send_lines, s_b += e.send_bytes, r_l += e.recv_lines, r_b += e.recv_bytes;
+        if (s_l < e.send_lines || s_b < e.send_bytes || r_l < e.recv_lines || r_b < e.recv_bytes) return -EINVAL;
+    }
+    // the own chunk is copied, so both sides of the all-to-all must agree on it
+    if (peers[rank].send_lines != peers[rank].recv_lines || peers[rank].send_bytes != peers[rank].recv_bytes)
+        return -EINVAL;
+    if (r_b > 0xFFFFFFFFull || r_l > 0xFFFFFFFFull) return -EINVAL;   // record offsets are u32
+    if (totals) totals[0] = s_l, totals[1] = s_b, totals[2] = r_l, totals[3] = r_b;
+    return 0;
+}
+
+inline int rebase_args(const sr_exchange_peer *peers, int world, RebaseArgs &a) {
+    if (world < 1 || world > kMaxOwners) return -EINVAL;
+    memset(&a, 0, sizeof(a));
+    uint64_t l = 0;
+    for (int q = 0; q < world; ++q) {
+        if (peers[q].recv_line0 != l || peers[q].recv_byte0 > 0xFFFFFFFFull) return -EINVAL;
+        a.line0[q] = (uint32_t)l;
+        a.byte0[q] = (uint32_t)peers[q].recv_byte0;
+        l += peers[q].recv_lines;
+    }
+    if (l > 0xFFFFFFFFull) return -EINVAL;
+    a.sources = (uint32_t)world;
+    a.n_lines = (uint32_t)l;
+    a.line0[world] = (uint32_t)l;
+    return 0;
+}
+
+// One exchange over a transport (sr_exchange_run): the plan, the peers' sends and receives in one
+// group (rank order; bytes then records; zero sizes skipped on both sides, since my send size to q
+// is q's receive size from me), the own chunk, then the rebase.
+inline int exchange_run(const sr_transport &t, int world, int rank, const uint64_t *sent, const uint64_t *received,
+                        const uint8_t *packed, const sr_record *packed_recs, uint8_t *recv_bytes,
+                        sr_record *recv_recs) {
+    if (!t.group_start || !t.group_end || !t.send || !t.recv || !t.copy || !t.rebase) return -EINVAL;
+    sr_exchange_peer peers[kMaxOwners];
+    uint64_t tot[4];
+    int rc = exchange_plan(world, rank, sent, received, peers, tot);
+    if (rc) return rc;
+    if ((tot[1] && !packed) || (tot[0] && !packed_recs) || (tot[3] && !recv_bytes) || (tot[2] && !recv_recs))
+        return -EINVAL;
+    if ((rc = t.group_start(t.user))) return rc;
+    int bad = 0;
+    for (int q = 0; q < world && !bad; ++q) {
+        if (q == rank) continue;
+        const sr_exchange_peer &e = peers[q];
+        if (e.send_bytes) bad = t.send(t.user, packed + e.send_byte0, e.send_bytes, q, 0);
+        if (!bad && e.recv_bytes) bad = t.recv(t.user, recv_bytes + e.recv_byte0, e.recv_bytes, q, 0);
+        if (!bad && e.send_lines)
+            bad = t.send(t.user, packed_recs + e.send_line0, e.send_lines * sizeof(sr_record), q, 1);
+        if (!bad && e.recv_lines)
+            bad = t.recv(t.user, recv_recs + e.recv_line0, e.recv_lines * sizeof(sr_record), q, 1);
+    }
+    rc = t.group_end(t.user);   // always closed, also after a failed post
+    if (bad) return bad;
+    if (rc) return rc;
+    const sr_exchange_peer &own = peers[rank];
+    if (own.send_bytes && (rc = t.copy(t.user, recv_bytes + own.recv_byte0, packed + own.send_byte0, own.send_bytes)))
+        return rc;
+    if (own.send_lines && (rc = t.copy(t.user, recv_recs + own.recv_line0, packed_recs + own.send_line0,
+                                       own.send_lines * sizeof(sr_record))))
+        return rc;
+    return tot[2] ? t.rebase(t.user, recv_recs, peers, world, tot[2]) : 0;
+}
 
 __global__ __launch_bounds__(256) void exchange_rebase_kernel(sr_record *recs, RebaseArgs a) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;

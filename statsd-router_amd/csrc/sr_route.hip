@@ -652,65 +652,78 @@ int sr_exchange_sizes(sr_ctx *ctx, sr_comm *comm, const uint64_t *d_owner_counts
     return 0;
 }
 
+static int rebase_launch(hipStream_t stream, sr_record *d_recs, const sr_exchange_peer *peers, int world) {
+    RebaseArgs a;
+    int rc = rebase_args(peers, world, a);
+    if (rc) return rc;
+    if (a.n_lines) {
+        hipLaunchKernelGGL(exchange_rebase_kernel, dim3((a.n_lines + 255u) / 256u), dim3(256), 0, stream, d_recs, a);
+        if (hipGetLastError() != hipSuccess) return -EIO;
+    }
+    return 0;
+}
+
+// The RCCL transport of sr_exchange_data: every call enqueued on the context's stream. Both chunk
+// kinds travel as bytes (the record chunk is 8 bytes per line on both sides of a pair).
+struct RcclTransport {
+    RcclApi *r;
+    sr_comm *comm;
+    hipStream_t stream;
+};
+
+static int rccl_group_start(void *u) { return ((RcclTransport *)u)->r->group_start() == 0 ? 0 : -EIO; }
+static int rccl_group_end(void *u) { return ((RcclTransport *)u)->r->group_end() == 0 ? 0 : -EIO; }
+static int rccl_send(void *u, const void *buf, size_t bytes, int peer, int) {
+    RcclTransport *t = (RcclTransport *)u;
+    return t->r->send(buf, bytes, kNcclUint8, peer, t->comm->nccl, t->stream) == 0 ? 0 : -EIO;
+}
+static int rccl_recv(void *u, void *buf, size_t bytes, int peer, int) {
+    RcclTransport *t = (RcclTransport *)u;
+    return t->r->recv(buf, bytes, kNcclUint8, peer, t->comm->nccl, t->stream) == 0 ? 0 : -EIO;
+}
+static int rccl_copy(void *u, void *dst, const void *src, size_t bytes) {
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ((RcclTransport *)u)->stream) == hipSuccess
+               ? 0 : -EIO;
+}
+static int rccl_rebase(void *u, sr_record *recs, const sr_exchange_peer *peers, int world, uint64_t) {
+    return rebase_launch(((RcclTransport *)u)->stream, recs, peers, world);
+}
+
 int sr_exchange_data(sr_ctx *ctx, sr_comm *comm, const uint8_t *d_packed, const sr_record *d_packed_recs,
                      const uint64_t *h_sent, const uint64_t *h_received, uint8_t *d_recv_bytes,
                      sr_record *d_recv_recs) {
     if (!ctx || !comm || !h_sent || !h_received) return -EINVAL;
     RcclApi *r = rccl_api();
     if (!r) return -ENOSYS;
-    const int G = comm->world;
-    uint64_t s_l = 0, s_b = 0, r_l = 0, r_b = 0;
-    RebaseArgs a;
-    memset(&a, 0, sizeof(a));
-    for (int q = 0; q < G; ++q) {
-        a.line0[q] = (uint32_t)r_l;
-        a.byte0[q] = (uint32_t)r_b;
-        s_l += h_sent[2 * q];
-        s_b += h_sent[2 * q + 1];
-        r_l += h_received[2 * q];
-        r_b += h_received[2 * q + 1];
-    }
-    if (r_b > 0xFFFFFFFFull || r_l > 0xFFFFFFFFull) return -EINVAL;   // record offsets are u32
-    if ((s_b && !d_packed) || (s_l && !d_packed_recs) || (r_b && !d_recv_bytes) || (r_l && !d_recv_recs))
-        return -EINVAL;
-    a.sources = (uint32_t)G;
-    a.n_lines = (uint32_t)r_l;
-    a.line0[G] = (uint32_t)r_l;
     (void)hipSetDevice(ctx->device);
-    if (r->group_start() != 0) return -EIO;
-    int bad = 0;
-    uint64_t so_l = 0, so_b = 0, ro_l = 0, ro_b = 0;
-    uint64_t self_so_l = 0, self_so_b = 0, self_ro_l = 0, self_ro_b = 0;
-    for (int q = 0; q < G; ++q) {
-        const uint64_t sl = h_sent[2 * q], sb = h_sent[2 * q + 1];
-        const uint64_t rl = h_received[2 * q], rb = h_received[2 * q + 1];
-        if (q == comm->rank) {   // our own chunk: a device copy below, not a send to ourselves
-            self_so_l = so_l, self_so_b = so_b, self_ro_l = ro_l, self_ro_b = ro_b;
-        } else {
-            if (sb) bad |= r->send(d_packed + so_b, sb, kNcclUint8, q, comm->nccl, ctx->stream);
-            if (rb) bad |= r->recv(d_recv_bytes + ro_b, rb, kNcclUint8, q, comm->nccl, ctx->stream);
-            if (sl) bad |= r->send(d_packed_recs + so_l, sl, kNcclUint64, q, comm->nccl, ctx->stream);
-            if (rl) bad |= r->recv(d_recv_recs + ro_l, rl, kNcclUint64, q, comm->nccl, ctx->stream);
-        }
-        so_l += sl;
-        so_b += sb;
-        ro_l += rl;
-        ro_b += rb;
-    }
-    if (r->group_end() != 0 || bad) return -EIO;
-    const uint64_t own_l = h_sent[2 * comm->rank], own_b = h_sent[2 * comm->rank + 1];
-    if (own_l != h_received[2 * comm->rank] || own_b != h_received[2 * comm->rank + 1]) return -EINVAL;
-    if ((own_b && hipMemcpyAsync(d_recv_bytes + self_ro_b, d_packed + self_so_b, own_b, hipMemcpyDeviceToDevice,
-                                 ctx->stream) != hipSuccess) ||
-        (own_l && hipMemcpyAsync(d_recv_recs + self_ro_l, d_packed_recs + self_so_l, own_l * sizeof(sr_record),
-                                 hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess))
-        return -EIO;
-    if (r_l) {
-        hipLaunchKernelGGL(exchange_rebase_kernel, dim3((uint32_t)((r_l + 255) / 256)), dim3(256), 0, ctx->stream,
-                           d_recv_recs, a);
-        if (hipGetLastError() != hipSuccess) return -EIO;
-    }
-    return 0;
+    RcclTransport rt{r, comm, ctx->stream};
+    const sr_transport t{&rt, rccl_group_start, rccl_group_end, rccl_send, rccl_recv, rccl_copy, rccl_rebase};
+    return exchange_run(t, comm->world, comm->rank, h_sent, h_received, d_packed, d_packed_recs, d_recv_bytes,
+                        d_recv_recs);
+}
+
+int sr_exchange_plan(int world, int rank, const uint64_t *h_sent, const uint64_t *h_received,
+                     sr_exchange_peer *peers, uint64_t *totals) {
+    uint64_t tot[4];
+    const int rc = exchange_plan(world, rank, h_sent, h_received, peers, tot);
+    if (!rc && totals) memcpy(totals, tot, sizeof(tot));
+    return rc;
+}
+
+int sr_exchange_run(const sr_transport *t, int world, int rank, const uint64_t *h_sent, const uint64_t *h_received,
+                    const uint8_t *packed, const sr_record *packed_recs, uint8_t *recv_bytes, sr_record *recv_recs) {
+    if (!t) return -EINVAL;
+    return exchange_run(*t, world, rank, h_sent, h_received, packed, packed_recs, recv_bytes, recv_recs);
+}
+
+int sr_exchange_rebase(sr_ctx *ctx, sr_record *d_recv_recs, const sr_exchange_peer *peers, int world) {
+    if (!ctx || !peers) return -EINVAL;
+    RebaseArgs a;
+    int rc = rebase_args(peers, world, a);
+    if (rc) return rc;
+    if (a.n_lines && !d_recv_recs) return -EINVAL;
+    (void)hipSetDevice(ctx->device);
+    return rebase_launch(ctx->stream, d_recv_recs, peers, world);
 }
 
 }  // extern "C"

@@ -68,6 +68,69 @@ def exchange_packed(packed_bytes: torch.Tensor, packed_recs: torch.Tensor, owner
     return _exchange(packed_bytes, packed_recs, owner_counts, group)[:3]
 
 
+class DistHostTransport:
+    """sr_transport over torch.distributed point-to-point calls on HOST memory (gloo): the C ABI's
+    exchange (sr_exchange_run: plan, grouped sends/receives, own chunk, rebase) with gloo in place of
+    RCCL, so the CPU tests drive the same C plan as sr_exchange_data. Sends and receives are posted
+    (isend/irecv) between group_start and group_end, which waits for all of them, like an RCCL group."""
+
+    def __init__(self, pkg, group=None):
+        self.pkg, self.group, self.pending = pkg, group, []
+        self.calls = []   # (kind, peer, tag, nbytes): what the plan asked for, in order
+
+    def _view(self, addr, n):
+        import ctypes
+        return torch.frombuffer((ctypes.c_uint8 * n).from_address(addr), dtype=torch.uint8)
+
+    def _global(self, peer):
+        return dist.get_global_rank(self.group, peer) if self.group is not None else peer
+
+    def group_start(self):
+        self.pending = []
+
+    def group_end(self):
+        for w in self.pending:
+            w.wait()
+        self.pending = []
+
+    def send(self, addr, n, peer, tag):
+        self.calls.append(("send", peer, tag, n))
+        self.pending.append(dist.isend(self._view(addr, n), self._global(peer), group=self.group, tag=tag))
+
+    def recv(self, addr, n, peer, tag):
+        self.calls.append(("recv", peer, tag, n))
+        self.pending.append(dist.irecv(self._view(addr, n), self._global(peer), group=self.group, tag=tag))
+
+    def copy(self, dst, src, n):
+        import ctypes
+        self.calls.append(("copy", -1, -1, n))
+        ctypes.memmove(dst, src, n)
+
+    def rebase(self, recs_addr, peers, n_lines):
+        self.calls.append(("rebase", -1, -1, n_lines))
+        self.pkg.Transport.rebase(self, recs_addr, peers, n_lines)
+
+
+def exchange_packed_c(pkg, packed_bytes: torch.Tensor, packed_recs: torch.Tensor, owner_counts: torch.Tensor,
+                      group=None, transport=None):
+    """exchange_packed through the C ABI's plan (sr_exchange_run) on host tensors: the split sizes by
+    all-to-all, then sr_exchange_run on a DistHostTransport. Returns (recv_bytes, recv_recs,
+    recv_counts [G, 2], transport)."""
+    G = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    sent = owner_counts.reshape(G, 2).contiguous()
+    received = torch.empty_like(sent)
+    dist.all_to_all_single(received, sent, group=group)
+    s, r = sent.numpy().astype(np.uint64), received.numpy().astype(np.uint64)
+    n_l, n_b = int(r[:, 0].sum()), int(r[:, 1].sum())
+    rb = torch.zeros(max(n_b, 1), dtype=torch.uint8)
+    rr = torch.zeros(max(n_l, 1), dtype=torch.int64)
+    t = transport or DistHostTransport(pkg, group)
+    pkg.exchange_run(t, G, rank, s, r, packed_bytes.data_ptr(), packed_recs.data_ptr(), rb.data_ptr(),
+                     rr.data_ptr())
+    return rb[:n_b], rr[:n_l], received, t
+
+
 class Regrouper:
     """Pack (HIP) + exchange for one Router context; buffers sized for one batch per slot.
 

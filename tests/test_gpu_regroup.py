@@ -1,5 +1,6 @@
-"""GPU: sr_pack_by_owner (HIP) against the oracle's restatement, and the Regrouper end to end on a
-one-rank RCCL group (the multi-rank exchange is covered with gloo in test_regroup_dist.py)."""
+"""GPU: sr_pack_by_owner (HIP) against the oracle's restatement, the Regrouper end to end on a one-rank
+RCCL group, and the C exchange: the rebase kernel on a 3-source receive buffer and sr_exchange_run over
+device memory with three ranks as threads (the multi-rank gloo exchange is in test_regroup_dist.py)."""
 from __future__ import annotations
 
 import importlib
@@ -246,3 +247,135 @@ def test_launch_regrouper_c_exchange(pkg, oracle, torch_stream):
         if comm is not None:
             comm.close()
         dist.destroy_process_group()
+
+
+def _three_rank_packs(pkg, oracle, world=3, n_shards=16):
+    """The oracle's launch packs of `world` ranks (rank world-1 has nothing valid to send)."""
+    alive = [0 if k % 7 == 3 else 1 for k in range(n_shards)]
+    packs = []
+    for r in range(world):
+        if r == world - 1:
+            datas = [np.frombuffer(pkg.frame_datagrams([b"no colon here\n", b"x\n"]), dtype=np.uint8)]
+        else:
+            datas = [pkg.gen_stream(1 << 18, [64, 256, 1024], seed=1300 + 10 * r + b, p_invalid=0.1).data
+                     for b in range(2)]
+        packs.append(oracle.pack_many_by_owner(datas, [oracle.route(d, n_shards, alive)[0] for d in datas], world))
+    return packs
+
+
+@pytest.mark.parametrize("owner", [0, 1, 2])
+def test_exchange_rebase_kernel_three_sources(pkg, oracle, owner, torch_stream):
+    """exchange_rebase_kernel (sr_exchange_rebase) on a synthetic 3-source receive buffer: the owner's
+    chunks of three ranks' packs concatenated with their offsets still relative to each source's chunk;
+    after the rebase every record addresses its line in the concatenated bytes."""
+    import torch
+
+    packs = _three_rank_packs(pkg, oracle)
+    received = np.stack([p[2][owner] for p in packs]).astype(np.uint64)
+    peers, tot = pkg.exchange_plan(3, owner, packs[owner][2].astype(np.uint64), received)
+    chunks_b, chunks_r = [], []
+    for s, (pb, pr, cnt) in enumerate(packs):
+        l0, b0 = int(cnt[:owner, 0].sum()), int(cnt[:owner, 1].sum())
+        chunks_b.append(pb[b0: b0 + int(cnt[owner, 1])])
+        chunks_r.append(pr[l0: l0 + int(cnt[owner, 0])])
+    rb = np.concatenate(chunks_b)
+    raw = np.concatenate(chunks_r)
+    assert int(tot[2]) == raw.size and int(tot[3]) == rb.size
+    exp = raw.copy()
+    for s in range(3):
+        a, n = int(peers[s]["recv_line0"]), int(peers[s]["recv_lines"])
+        exp["offset"][a: a + n] += np.uint32(sum(int(packs[q][2][owner, 1]) for q in range(s)))
+    d = torch.from_numpy(raw.view(np.int64).copy()).to("cuda")
+    with pkg.Router(16, 1 << 16) as r:
+        r.set_stream(torch_stream.cuda_stream)
+        r.exchange_rebase(d.data_ptr(), peers)
+        r.sync()
+    got = d.cpu().numpy().view(pkg.RECORD_DTYPE)
+    assert np.array_equal(got, exp)
+    # every rebased record addresses its own line (the oracle's per-owner stream, source by source)
+    lines = [bytes(pb[int(cnt[:owner, 1].sum()) + x["offset"]:][: x["length"]])
+             for pb, pr, cnt in packs for x in pr[int(cnt[:owner, 0].sum()):][: int(cnt[owner, 0])]]
+    assert [bytes(rb[x["offset"]: x["offset"] + x["length"]]) for x in got] == lines
+
+
+def test_exchange_run_device_three_ranks(pkg, oracle):
+    """sr_exchange_run over device memory with three ranks as threads of one process (sends through
+    host mailboxes by hipMemcpy, own chunk hipMemcpy, rebase = the shipped kernel via
+    sr_exchange_rebase): every owner's receive buffers equal the oracle's per-owner stream."""
+    import ctypes
+    import threading
+
+    import torch
+
+    hip = ctypes.CDLL("libamdhip64.so.7")   # the runtime torch (and libsr_route.so) already loaded
+    hip.hipMemcpy.restype = ctypes.c_int
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    world = 3
+    packs = _three_rank_packs(pkg, oracle, world)
+    box, cond, out, errs = {}, threading.Condition(), {}, {}
+
+    class DeviceMailbox(pkg.Transport):
+        def __init__(self, rank, router):
+            self.rank, self.router, self.posted = rank, router, []
+
+        def group_start(self):
+            self.posted = []
+
+        def send(self, addr, n, peer, tag):
+            blob = ctypes.create_string_buffer(n)
+            assert hip.hipMemcpy(ctypes.addressof(blob), addr, n, 4) == 0
+            with cond:
+                box.setdefault((self.rank, peer, tag), []).append(blob)
+                cond.notify_all()
+
+        def recv(self, addr, n, peer, tag):
+            self.posted.append((addr, n, peer, tag))
+
+        def group_end(self):
+            for addr, n, peer, tag in self.posted:
+                with cond:
+                    assert cond.wait_for(lambda: box.get((peer, self.rank, tag)), timeout=60)
+                    blob = box[(peer, self.rank, tag)].pop(0)
+                assert len(blob) == n and hip.hipMemcpy(addr, ctypes.addressof(blob), n, 4) == 0
+
+        def copy(self, dst, src, n):
+            assert hip.hipMemcpy(dst, src, n, 4) == 0
+
+        def rebase(self, recs_addr, peers, n_lines):
+            self.router.exchange_rebase(recs_addr, peers)
+            self.router.sync()
+
+    def rank_main(r):
+        try:
+            torch.cuda.set_device(0)
+            pb, pr, cnt = packs[r]
+            sent = cnt.astype(np.uint64)
+            received = np.stack([packs[s][2][r] for s in range(world)]).astype(np.uint64)
+            n_l, n_b = int(received[:, 0].sum()), int(received[:, 1].sum())
+            d_pb = torch.from_numpy(np.concatenate([pb, np.zeros(4, np.uint8)])).to("cuda")
+            d_pr = torch.from_numpy(np.concatenate([pr, np.zeros(1, pkg.RECORD_DTYPE)]).view(np.int64).copy()).to("cuda")
+            d_rb = torch.full((n_b + 64,), 0xCD, dtype=torch.uint8, device="cuda")
+            d_rr = torch.zeros(max(n_l, 1), dtype=torch.int64, device="cuda")
+            torch.cuda.synchronize()
+            with pkg.Router(16, 1 << 16) as router:
+                pkg.exchange_run(DeviceMailbox(r, router), world, r, sent, received, d_pb.data_ptr(),
+                                 d_pr.data_ptr(), d_rb.data_ptr(), d_rr.data_ptr())
+                router.sync()
+            out[r] = (d_rb.cpu().numpy(), d_rr.cpu().numpy().view(pkg.RECORD_DTYPE)[:n_l], n_b)
+        except Exception as e:   # noqa: BLE001
+            errs[r] = e
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not errs, errs
+    for r in range(world):
+        rb, rr, n_b = out[r]
+        assert (rb[n_b:] == 0xCD).all()
+        eb = np.concatenate([packs[s][0][int(packs[s][2][:r, 1].sum()):][: int(packs[s][2][r, 1])] for s in range(world)])
+        assert np.array_equal(rb[:n_b], eb)
+        lines = [bytes(pb[int(cnt[:r, 1].sum()) + x["offset"]:][: x["length"]])
+                 for pb, pr, cnt in packs for x in pr[int(cnt[:r, 0].sum()):][: int(cnt[r, 0])]]
+        assert [bytes(rb[x["offset"]: x["offset"] + x["length"]]) for x in rr] == lines

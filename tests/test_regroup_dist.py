@@ -1,7 +1,8 @@
-"""Multi-rank regroup on CPU with gloo: the product's exchange step
-(statsd-router_amd/regroup.py: all-to-all of split sizes, packed bytes and records, offset rebase)
-between world_size 2 and 3 process groups. The pack input comes from the oracle's restatement of
-sr_pack_by_owner (the HIP pack itself is checked against it in test_gpu_regroup.py)."""
+"""Multi-rank regroup on CPU with gloo between world_size 2, 3 and 4 process groups:
+the C ABI's exchange (sr_exchange_run: the plan, call sequence and rebase of sr_exchange_data, with
+gloo point-to-point in place of RCCL) and the torch.distributed exchange (regroup.exchange_packed).
+The pack input comes from the oracle's restatement of sr_pack_by_owner (the HIP pack itself is checked
+against it in test_gpu_regroup.py)."""
 from __future__ import annotations
 
 import importlib
@@ -35,7 +36,7 @@ def _inputs(pkg, oracle, rank, n_shards, alive, b=0):
     return data, recs
 
 
-def _worker(rank, world, port, n_shards, q, nb=1):
+def _worker(rank, world, port, n_shards, q, nb=1, exchange="torch"):
     try:
         sys.path.insert(0, REPO)
         sys.path.insert(0, os.path.join(REPO, "oracle"))
@@ -54,8 +55,18 @@ def _worker(rank, world, port, n_shards, q, nb=1):
             pb, pr, cnt = oracle.pack_by_owner(ins[0][0], ins[0][1], world)
         else:   # a launch's batches packed together (sr_pack_many_by_owner's layout)
             pb, pr, cnt = oracle.pack_many_by_owner([d for d, _ in ins], [r for _, r in ins], world)
-        rb, rr, rc = rg.exchange_packed(torch.from_numpy(pb), torch.from_numpy(pr.view(np.int64)),
-                                        torch.from_numpy(cnt), None)
+        tb, tr = torch.from_numpy(pb), torch.from_numpy(pr.view(np.int64))
+        if exchange == "c":   # the C ABI's plan and calls (sr_exchange_run) on gloo point-to-point
+            rb, rr, rc, t = rg.exchange_packed_c(pkg, tb, tr, torch.from_numpy(cnt), None)
+            posts = [c for c in t.calls if c[0] in ("send", "recv")]
+            assert [c[1] for c in posts] == sorted(c[1] for c in posts) and rank not in [c[1] for c in posts]
+            sizes = {(c[0], c[1], c[2]): c[3] for c in posts}
+            for p in range(world):   # what the plan posted = the split sizes, both directions
+                if p != rank:
+                    assert sizes.get(("send", p, 0), 0) == cnt[p, 1] and sizes.get(("send", p, 1), 0) == 8 * cnt[p, 0]
+                    assert sizes.get(("recv", p, 0), 0) == int(rc[p, 1]) and sizes.get(("recv", p, 1), 0) == 8 * int(rc[p, 0])
+        else:                 # the torch.distributed exchange (regroup.exchange_packed)
+            rb, rr, rc = rg.exchange_packed(tb, tr, torch.from_numpy(cnt), None)
         rb, rr = rb.numpy(), rr.numpy().view(pkg.RECORD_DTYPE)
         # expected: every source's valid lines of the shards this rank owns, source by source
         exp_lines, exp_routes = [], []
@@ -78,12 +89,15 @@ def _worker(rank, world, port, n_shards, q, nb=1):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world,n_shards,nb", [(2, 64, 1), (3, 16, 1), (2, 1, 1), (2, 64, 3), (3, 16, 2)])
-def test_regroup_exchange_gloo(world, n_shards, nb):
+@pytest.mark.parametrize("exchange", ["c", "torch"])
+@pytest.mark.parametrize("world,n_shards,nb", [(2, 64, 1), (3, 16, 1), (2, 1, 1), (2, 64, 3), (3, 16, 2), (4, 64, 1)])
+def test_regroup_exchange_gloo(world, n_shards, nb, exchange):
+    """exchange "c": sr_exchange_run (the plan and call sequence of sr_exchange_data) over gloo;
+    "torch": regroup.exchange_packed. Both against the oracle's per-owner streams."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_shards, q, nb)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_shards, q, nb, exchange)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
