@@ -260,13 +260,20 @@ def main(argv=None):
         # the dominant kernel's achieved HBM rate: algorithmic bytes (the framed bytes, read once)
         # of the timed launches on this GPU over their GPU time
         achieved = steps_bytes / (region_ms * 1e-3) / 1e9
-        traffic = None
+        traffic, traffic_src = None, None
         tj = args.traffic_json
         if tj and os.path.exists(tj):
             with open(tj) as f:
                 tr = json.load(f)
-            if tr.get("config") == args.config:
+            # counter bytes of a rocprofv3 --pmc run (tools/pmc_summary.py) count only when they were
+            # measured on this very build of the library and configuration
+            lib_sha = hashlib.sha256(open(pkg.ROUTE_LIB, "rb").read()).hexdigest()
+            if tr.get("config") == args.config and tr.get("lib_sha256") == lib_sha:
                 traffic = tr.get("hbm_bytes_per_launch")
+                traffic_src = f"{os.path.relpath(tj, REPO)} (rocprofv3 --pmc of this build, lib sha256 {lib_sha[:12]})"
+            else:
+                traffic_src = (f"{os.path.relpath(tj, REPO)} is for config {tr.get('config')} / lib "
+                               f"{str(tr.get('lib_sha256'))[:12]}, not this build: not reported")
         result = {
             "metric": "M metrics/s parsed+hashed, device-resident (GiB/s and HBM roofline alongside)",
             "value": round(total_lines / wall_max / 1e6, 3),
@@ -304,6 +311,7 @@ def main(argv=None):
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": "route_kernel",
                 "read_ceiling": dict(ceiling, frac_of_ceiling=round(achieved / ceiling["achieved"], 4))
                 if ceiling.get("achieved") else ceiling,
@@ -339,11 +347,13 @@ def main(argv=None):
         # a collective that never completes (a peer lost, a transport stuck) must not take the main
         # line with it: past the deadline every rank prints what it has and leaves
         def give_up():
+            print(f"bench.py rank {rank}: regroup leg timed out after {args.regroup_timeout:.0f} s", file=sys.stderr)
             if rank == 0:
                 result["regroup"] = {"error": f"timed out after {args.regroup_timeout:.0f} s"}
             emit(result)
             sys.stderr.flush()
-            os._exit(0)
+            json_out.flush()
+            os._exit(3)   # the line is out; the exit status still says the run did not finish cleanly
 
         dog = threading.Timer(args.regroup_timeout, give_up)
         dog.daemon = True
@@ -600,16 +610,19 @@ def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, de
     d_counts = torch.zeros((M, 3), dtype=torch.int64, device=dev)
     d_fill = torch.zeros((M, shards), dtype=torch.int16, device=dev)
     d_fout = torch.zeros((M, shards), dtype=torch.int16, device=dev)
+    # the probed-dead bitmap of every batch, as the router asks for it (sr-main.c:106; with every shard
+    # alive the route launch skips it)
+    d_pd = torch.zeros((M, max((shards + 63) // 64, 1)), dtype=torch.int64, device=dev)
     base = d_in.data_ptr()
 
     def route():
         router.route_device_many([(base + b * batch_bytes, sizes[b], d_rec[b].data_ptr(), max_lines, None,
-                                   d_cnt[b].data_ptr()) for b in range(M)])
+                                   d_cnt[b].data_ptr(), d_pd[b].data_ptr()) for b in range(M)])
 
     def pack():   # the batches of M data threads: independent pending bytes, one set of launches
-        router.pack_packets_many([(d_rec[b].data_ptr(), d_cnt[b].data_ptr(), max_lines, d_fill[b].data_ptr(), 0,
-                                   d_srt[b].data_ptr(), d_pk[b].data_ptr(), mp, d_counts[b].data_ptr(),
-                                   d_fout[b].data_ptr()) for b in range(M)])
+        router.pack_packets_many([(d_rec[b].data_ptr(), d_cnt[b].data_ptr(), max_lines, d_fill[b].data_ptr(),
+                                   d_pd[b].data_ptr(), d_srt[b].data_ptr(), d_pk[b].data_ptr(), mp,
+                                   d_counts[b].data_ptr(), d_fout[b].data_ptr()) for b in range(M)])
 
     with torch.cuda.stream(stream):
         route()
@@ -638,8 +651,10 @@ def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, de
             "ms_per_launch": round(res["route_pack"], 4), "route_only_ms": round(res["route_only"], 4),
             "packing_ms": round(res["route_pack"] - res["route_only"], 4),
             "packets_per_launch": packets,
-            "note": (f"one route launch over {M} batches + one sr_pack_packets_many over them (regroup by downstream, "
-                     f"next-fit 1450-byte packets), one graph, {reps} replays")}
+            "probed_dead_shards": int(sum(bin(int(w) & (2**64 - 1)).count("1") for w in d_pd[0].tolist())),
+            "note": (f"one route launch over {M} batches with their probed-dead bitmaps (sr-main.c:106, replayed when "
+                     f"a shard is dead) + one sr_pack_packets_many over them (regroup by downstream, next-fit 1450-byte "
+                     f"packets), one graph, {reps} replays")}
 
 
 def e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M, groups=24):

@@ -45,12 +45,14 @@ struct sr_core {
     void *user;
     /* per-batch buffers (page-locked) */
     size_t max_batch;
-    uint8_t *in;
+    uint8_t *in[2];                          /* the two slots' framed datagrams                 */
+    const uint8_t *in_flight_bytes;          /* the framed bytes of the batch in flight          */
+    int in_flight;                           /* slot whose batch is on the GPU, or -1            */
+    int host_fills;                          /* the host changed pending buffers since the last  */
+                                             /* submission: upload them with the next one         */
     uint16_t *fill16;
-    sr_record *sorted;
+    sr_record *sorted;                       /* the ping names' records (sr_route_batch)         */
     size_t sorted_cap;
-    sr_packet *packets;
-    size_t packets_cap;
     uint64_t *probed;
     struct iovec *iov;
     char *msg;
@@ -117,9 +119,9 @@ static void build_names(sr_core *c, const sr_core_config *cfg) {
 void sr_core_close(sr_core *c) {
     if (!c) return;
     if (c->ctx) sr_close(c->ctx);
-    sr_free_host(c->in);
+    sr_free_host(c->in[0]);
+    sr_free_host(c->in[1]);
     sr_free_host(c->sorted);
-    sr_free_host(c->packets);
     free(c->fill16);
     free(c->probed);
     free(c->iov);
@@ -151,8 +153,8 @@ int sr_core_open(sr_core **out, const sr_core_config *cfg, sr_core_emit_fn emit,
         sr_core_close(c);
         return rc;
     }
-    c->sorted_cap = cfg->max_batch_bytes;   /* never more lines than bytes */
-    c->packets_cap = (size_t)SR_MAX_PACKETS(cfg->max_batch_bytes, c->n);
+    c->in_flight = -1;
+    c->host_fills = 1;
     c->msg_cap = 3 * SR_DATA_BUF_SIZE;
     c->ds = calloc(c->n, sizeof(ds_state));
     c->alive = calloc(c->nwords, sizeof(uint64_t));
@@ -162,11 +164,12 @@ int sr_core_open(sr_core **out, const sr_core_config *cfg, sr_core_emit_fn emit,
     c->msg = malloc(c->msg_cap);
     c->ping_cap = ((size_t)c->n + 1) * (SR_METRIC_SIZE + 8);
     c->ping = malloc(c->ping_cap);
-    c->in = sr_alloc_host(cfg->max_batch_bytes);
+    c->sorted_cap = (size_t)c->n + 1;   /* the ping batch: one line per name */
+    c->in[0] = sr_alloc_host(cfg->max_batch_bytes);
+    c->in[1] = sr_alloc_host(cfg->max_batch_bytes);
     c->sorted = sr_alloc_host(c->sorted_cap * sizeof(sr_record));
-    c->packets = sr_alloc_host(c->packets_cap * sizeof(sr_packet));
-    if (!c->ds || !c->alive || !c->fill16 || !c->probed || !c->iov || !c->msg || !c->ping || !c->in || !c->sorted ||
-        !c->packets) {
+    if (!c->ds || !c->alive || !c->fill16 || !c->probed || !c->iov || !c->msg || !c->ping || !c->in[0] ||
+        !c->in[1] || !c->sorted) {
         sr_core_close(c);
         return -ENOMEM;
     }
@@ -182,15 +185,19 @@ int sr_core_open(sr_core **out, const sr_core_config *cfg, sr_core_emit_fn emit,
 
 int sr_core_set_alive(sr_core *c, const uint64_t *alive) {
     if (!c || !alive) return -EINVAL;
+    int rc = sr_core_drain(c);
+    if (rc) return rc;
     memcpy(c->alive, alive, c->nwords * sizeof(uint64_t));
     if (c->n & 63) c->alive[c->nwords - 1] &= (1ull << (c->n & 63)) - 1;
     return sr_set_alive(c->ctx, c->alive);
 }
 
-uint8_t *sr_core_batch_buffer(sr_core *c, size_t *cap) {
-    if (!c) return NULL;
+uint8_t *sr_core_batch_buffer(sr_core *c, size_t *cap) { return sr_core_slot_buffer(c, 0, cap); }
+
+uint8_t *sr_core_slot_buffer(sr_core *c, int slot, size_t *cap) {
+    if (!c || slot < 0 || slot > 1) return NULL;
     if (cap) *cap = c->max_batch;
-    return c->in;
+    return c->in[slot];
 }
 
 static void drop_probed(sr_core *c) {
@@ -214,34 +221,31 @@ static void warn_line(sr_core *c, const uint8_t *framed, const sr_record *r) {
     }
 }
 
-int sr_core_route(sr_core *c, const uint8_t *framed, size_t nbytes) {
-    if (!c || (nbytes && !framed) || nbytes > c->max_batch) return -EINVAL;
-    if (nbytes == 0) return 0;
-    for (uint32_t s = 0; s < c->n; s++) c->fill16[s] = (uint16_t)c->ds[s].fill;
-    size_t nr = 0, nv = 0, np = 0;
-    int rc = sr_route_pack_batch(c->ctx, framed, nbytes, c->fill16, c->sorted, c->sorted_cap, &nr, &nv, c->packets,
-                                 c->packets_cap, &np, c->probed);
-    if (rc) return rc;
+/* The host's half of a batch (udp_read_cb's per-line side effects, sr-main.c:175-189, for a whole
+ * batch): drop probed dead buffers, WARN lines in input order, then the packets per downstream. */
+static void complete(sr_core *c, const uint8_t *framed, const sr_pack_result *r) {
+    memcpy(c->probed, r->probed_dead, c->nwords * sizeof(uint64_t));
     drop_probed(c);
     if (c->log_level <= SR_WARN)
-        for (size_t i = nv; i < nr; i++) warn_line(c, framed, &c->sorted[i]);
-    for (size_t q = 0; q < np; q++) {
-        const sr_packet *p = &c->packets[q];
+        for (size_t i = r->n_valid; i < r->n_records; i++) warn_line(c, framed, &r->sorted[i]);
+    for (size_t q = 0; q < r->n_packets; q++) {
+        const sr_packet *p = &r->packets[q];
         ds_state *d = &c->ds[p->shard];
-        const sr_record *r = c->sorted + p->first;
+        const sr_record *rec = r->sorted + p->first;
         if (p->open) {
             /* the new active buffer: the carried bytes (already in place) + this batch's lines */
             uint32_t f = p->carry;
             for (uint32_t k = 0; k < p->nlines; k++) {
-                memcpy(d->pending + f, framed + r[k].offset, r[k].length);
-                f += r[k].length;
+                memcpy(d->pending + f, framed + rec[k].offset, rec[k].length);
+                f += rec[k].length;
             }
             d->fill = f;
             continue;
         }
         int iv = 0;
         if (p->carry) c->iov[iv++] = (struct iovec){d->pending, p->carry};
-        for (uint32_t k = 0; k < p->nlines; k++) c->iov[iv++] = (struct iovec){(void *)(framed + r[k].offset), r[k].length};
+        for (uint32_t k = 0; k < p->nlines; k++)
+            c->iov[iv++] = (struct iovec){(void *)(framed + rec[k].offset), rec[k].length};
         const uint32_t bytes = (uint32_t)p->carry + p->length;
         d->packets += 1;
         d->traffic = (int32_t)((uint32_t)d->traffic + bytes);
@@ -249,11 +253,67 @@ int sr_core_route(sr_core *c, const uint8_t *framed, size_t nbytes) {
         d->fill = 0;
     }
     if (c->flush) c->flush(c->user);
+}
+
+/* Start a batch on the GPU; the pending bytes are the device's own unless the host changed them. */
+static int submit(sr_core *c, int slot, const uint8_t *framed, size_t nbytes) {
+    const uint16_t *fill = NULL;
+    if (c->host_fills) {   /* nothing is in flight here: the host's fills are current */
+        for (uint32_t s = 0; s < c->n; s++) c->fill16[s] = (uint16_t)c->ds[s].fill;
+        fill = c->fill16;
+    }
+    int rc = sr_route_pack_submit(c->ctx, slot, framed, nbytes, fill);
+    if (rc) return rc;
+    c->host_fills = 0;
     return 0;
+}
+
+static int finish(sr_core *c, int slot, const uint8_t *framed) {
+    sr_pack_result r;
+    int rc = sr_route_pack_result(c->ctx, slot, &r);
+    if (rc) {
+        c->host_fills = 1;   /* the device's chain is no longer what the host holds */
+        return rc;
+    }
+    complete(c, framed, &r);
+    return 0;
+}
+
+int sr_core_drain(sr_core *c) {
+    if (!c) return -EINVAL;
+    if (c->in_flight < 0) return 0;
+    const int slot = c->in_flight;
+    c->in_flight = -1;
+    return finish(c, slot, c->in_flight_bytes);
+}
+
+int sr_core_submit(sr_core *c, int slot, size_t nbytes) {
+    if (!c || slot < 0 || slot > 1 || nbytes > c->max_batch) return -EINVAL;
+    if (c->in_flight == slot) return -EBUSY;
+    if (nbytes == 0) return 0;
+    int rc = submit(c, slot, c->in[slot], nbytes);
+    if (rc) return rc;
+    const int prev = c->in_flight;
+    const uint8_t *prev_bytes = c->in_flight_bytes;
+    c->in_flight = slot;
+    c->in_flight_bytes = c->in[slot];
+    return prev >= 0 ? finish(c, prev, prev_bytes) : 0;
+}
+
+int sr_core_route(sr_core *c, const uint8_t *framed, size_t nbytes) {
+    if (!c || (nbytes && !framed) || nbytes > c->max_batch) return -EINVAL;
+    int rc = sr_core_drain(c);
+    if (rc) return rc;
+    if (nbytes == 0) return 0;
+    if ((rc = submit(c, 0, framed, nbytes))) return rc;
+    return finish(c, 0, framed);
 }
 
 int sr_core_flush_timer(sr_core *c) {
     if (!c) return -EINVAL;
+    int rc = sr_core_drain(c);
+    if (rc) return rc;
+    c->host_fills = 1;
     for (uint32_t s = 0; s < c->n; s++)
         if (c->ds[s].fill > 0) schedule_flush(c, s); /* sr-main.c:199-203 */
     if (c->flush) c->flush(c->user);
@@ -262,6 +322,9 @@ int sr_core_flush_timer(sr_core *c) {
 
 int sr_core_ping(sr_core *c) {
     if (!c) return -EINVAL;
+    int rc = sr_core_drain(c);
+    if (rc) return rc;
+    c->host_fills = 1;
     /* The shard of a ping line depends only on its name (the bytes before ':') and the alive bits,
      * so the n + 1 names are routed on the GPU in one batch first; the texts, whose counters change
      * as earlier lines are pushed, are formatted afterwards in the reference's order. */
@@ -275,7 +338,7 @@ int sr_core_ping(sr_core *c) {
     }
     if (pos > c->max_batch) return -ENOSPC;
     size_t nr = 0;
-    int rc = sr_route_batch(c->ctx, b, pos, c->sorted, c->sorted_cap, &nr, NULL);
+    rc = sr_route_batch(c->ctx, b, pos, c->sorted, c->sorted_cap, &nr, NULL);
     if (rc) return rc;
     if (nr != c->n + 1) return -EIO;
     if ((rc = sr_last_probed_dead(c->ctx, c->probed))) return rc;

@@ -53,6 +53,7 @@ typedef struct sr_config {
     /* GPU side */
     size_t batch_bytes;                         /* framed bytes per sr_core_route call */
     int n_devices;
+    int require_gpu;                            /* a data thread without a GPU ends the process */
     /* alive bits published by the health checker to the data threads */
     _Atomic uint64_t alive_gen;
     _Atomic uint64_t *alive_words;

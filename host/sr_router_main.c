@@ -17,6 +17,7 @@
  */
 #define _GNU_SOURCE
 #include <errno.h>
+#include <signal.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -27,6 +28,7 @@
 
 #define RECV_VLEN 256      /* datagrams per recvmmsg call */
 #define SEND_VLEN 512      /* packets per sendmmsg call */
+#define MAX_BATCHES_PER_READ 4   /* full batches per read event before the loop runs its timers again */
 
 typedef struct data_thread {
     sr_thread *t;
@@ -37,9 +39,10 @@ typedef struct data_thread {
     sr_core *core;
     int sock_in;
     int *sock_out;
-    /* ingress */
-    uint8_t *batch;          /* page-locked, framed datagrams back to back */
+    /* ingress: two page-locked batches (the core's slots); the one being filled is `slot` */
+    uint8_t *batch;          /* framed datagrams back to back: the buffer of `slot` */
     size_t cap, len;
+    int slot;
     struct mmsghdr rmsg[RECV_VLEN];
     struct iovec riov[RECV_VLEN];
     /* egress: per outgoing socket, packets staged for one sendmmsg */
@@ -110,12 +113,27 @@ static void refresh_alive(data_thread *d) {
     if (rc) sr_log(SR_ERROR, "%s: sr_core_set_alive() failed %s", "data_pipe_thread", strerror(-rc));
 }
 
-static void route_batch(data_thread *d) {
+/* A read event's batches go to the GPU while the next ones are received (sr_core_submit: slot k routes
+ * while slot k^1 fills and the batch before it is walked and sent); the event ends with the last batch
+ * drained, so a lone datagram still costs one GPU round trip. */
+static void submit_batch(data_thread *d) {
     if (!d->len) return;
     refresh_alive(d);
-    int rc = sr_core_route(d->core, d->batch, d->len);
-    if (rc) sr_log(SR_ERROR, "%s: sr_core_route() failed %s", "udp_read_cb", strerror(-rc));
+    int rc = sr_core_submit(d->core, d->slot, d->len);
+    if (rc) sr_log(SR_ERROR, "%s: sr_core_submit() failed %s", "udp_read_cb", strerror(-rc));
+    d->slot ^= 1;
+    d->batch = sr_core_slot_buffer(d->core, d->slot, &d->cap);
     d->len = 0;
+}
+
+static void drain(data_thread *d) {
+    int rc = sr_core_drain(d->core);
+    if (rc) sr_log(SR_ERROR, "%s: sr_core_drain() failed %s", "udp_read_cb", strerror(-rc));
+}
+
+static void route_batch(data_thread *d) {
+    submit_batch(d);
+    drain(d);
 }
 
 static void udp_read_cb(struct ev_loop *loop, ev_io *w, int revents) {
@@ -125,8 +143,15 @@ static void udp_read_cb(struct ev_loop *loop, ev_io *w, int revents) {
         sr_log(SR_WARN, "%s: invalid event %s", "udp_read_cb", strerror(errno));
         return;
     }
+    /* Under sustained load the socket never drains: after MAX_BATCHES_PER_READ full batches the event
+     * returns to the loop (the socket is still readable, so it comes straight back), and the flush,
+     * ping and alive updates run in between, as they do between the reference's one-datagram reads. */
+    int batches = 0;
     for (;;) {
-        if (d->cap - d->len < (size_t)RECV_VLEN * SR_DATA_BUF_SIZE) route_batch(d);
+        if (d->cap - d->len < (size_t)RECV_VLEN * SR_DATA_BUF_SIZE) {
+            submit_batch(d);
+            if (++batches >= MAX_BATCHES_PER_READ) break;
+        }
         /* datagram j lands in its own 4096-byte slot after the batch's end, capped at 4095 bytes
          * like recv(fd, buffer, DATA_BUF_SIZE - 1) (sr-main.c:163), then is moved down and framed */
         for (int j = 0; j < RECV_VLEN; j++) {
@@ -172,6 +197,16 @@ static void ping_timer_cb(struct ev_loop *loop, ev_periodic *p, int revents) {
     if (rc) sr_log(SR_ERROR, "%s: sr_core_ping() failed %s", "ping_cb", strerror(-rc));
 }
 
+/* a data thread that cannot route: the process ends (status 1) unless SR_REQUIRE_GPU=0 */
+static void *thread_fail(data_thread *d, int gpu) {
+    if (d->sock_in >= 0) close(d->sock_in);
+    if (gpu && d->c->require_gpu) {
+        fflush(stdout);
+        _exit(1);
+    }
+    return NULL;
+}
+
 void *sr_data_thread(void *arg) {
     sr_thread *t = arg;
     sr_config *c = t->config;
@@ -180,45 +215,8 @@ void *sr_data_thread(void *arg) {
     if (!d) return NULL;
     d->t = t;
     d->c = c;
-    d->loop = ev_loop_new(0);
-    d->sock_in = socket(PF_INET, SOCK_DGRAM, 0);
-    if (d->sock_in < 0) {
-        sr_log(SR_ERROR, "%s: socket_in socket() error %s", fn, strerror(errno));
-        return NULL;
-    }
-    struct sockaddr_in addr;
-    memset(&addr, 0, sizeof(addr));
-    addr.sin_family = AF_INET;
-    addr.sin_port = htons((uint16_t)c->data_port);
-    addr.sin_addr.s_addr = INADDR_ANY;
-    int one = 1;
-    if (setsockopt(d->sock_in, SOL_SOCKET, SO_REUSEPORT, &one, sizeof(one)) != 0) {
-        sr_log(SR_ERROR, "%s: setsockopt() failed %s", fn, strerror(errno));
-        return NULL;
-    }
-    int rcvbuf = 32 << 20;
-    setsockopt(d->sock_in, SOL_SOCKET, SO_RCVBUF, &rcvbuf, sizeof(rcvbuf));
-    if (bind(d->sock_in, (struct sockaddr *)&addr, sizeof(addr)) != 0) {
-        sr_log(SR_ERROR, "%s: bind() failed %s", fn, strerror(errno));
-        return NULL;
-    }
-    d->nout = c->socket_out_num;
-    d->sock_out = calloc((size_t)d->nout, sizeof(int));
-    d->smsg = calloc((size_t)d->nout * SEND_VLEN, sizeof(struct mmsghdr));
-    d->siov = calloc((size_t)d->nout * SEND_VLEN, sizeof(struct iovec));
-    d->stage = malloc((size_t)d->nout * SEND_VLEN * SR_DOWNSTREAM_BUF_SIZE);
-    d->nq = calloc((size_t)d->nout, sizeof(int));
-    d->alive = calloc((size_t)(c->downstream_num + 63) / 64, sizeof(uint64_t));
-    if (!d->sock_out || !d->smsg || !d->siov || !d->stage || !d->nq || !d->alive) {
-        sr_log(SR_ERROR, "%s: malloc() failed %s", fn, strerror(errno));
-        return NULL;
-    }
-    for (int i = 0; i < d->nout; i++) {
-        if ((d->sock_out[i] = socket(AF_INET, SOCK_DGRAM, IPPROTO_UDP)) < 0) {
-            sr_log(SR_ERROR, "%s: socket_out socket() error %s", fn, strerror(errno));
-            return NULL;
-        }
-    }
+    d->sock_in = -1;
+    /* the GPU context first: no socket takes a share of the data port before this thread can route */
     sr_core_config cc;
     memset(&cc, 0, sizeof(cc));
     cc.device = c->n_devices > 0 ? t->index % c->n_devices : 0;
@@ -233,9 +231,49 @@ void *sr_data_thread(void *arg) {
     int rc = sr_core_open(&d->core, &cc, on_emit, on_log, on_flush, d);
     if (rc) {
         sr_log(SR_ERROR, "%s: sr_core_open() failed %s", fn, strerror(-rc));
-        return NULL;
+        return thread_fail(d, 1);
     }
-    d->batch = sr_core_batch_buffer(d->core, &d->cap);
+    d->slot = 0;
+    d->batch = sr_core_slot_buffer(d->core, 0, &d->cap);
+    d->loop = ev_loop_new(0);
+    d->sock_in = socket(PF_INET, SOCK_DGRAM, 0);
+    if (d->sock_in < 0) {
+        sr_log(SR_ERROR, "%s: socket_in socket() error %s", fn, strerror(errno));
+        return thread_fail(d, 0);
+    }
+    struct sockaddr_in addr;
+    memset(&addr, 0, sizeof(addr));
+    addr.sin_family = AF_INET;
+    addr.sin_port = htons((uint16_t)c->data_port);
+    addr.sin_addr.s_addr = INADDR_ANY;
+    int one = 1;
+    if (setsockopt(d->sock_in, SOL_SOCKET, SO_REUSEPORT, &one, sizeof(one)) != 0) {
+        sr_log(SR_ERROR, "%s: setsockopt() failed %s", fn, strerror(errno));
+        return thread_fail(d, 0);
+    }
+    int rcvbuf = 32 << 20;
+    setsockopt(d->sock_in, SOL_SOCKET, SO_RCVBUF, &rcvbuf, sizeof(rcvbuf));
+    if (bind(d->sock_in, (struct sockaddr *)&addr, sizeof(addr)) != 0) {
+        sr_log(SR_ERROR, "%s: bind() failed %s", fn, strerror(errno));
+        return thread_fail(d, 0);
+    }
+    d->nout = c->socket_out_num;
+    d->sock_out = calloc((size_t)d->nout, sizeof(int));
+    d->smsg = calloc((size_t)d->nout * SEND_VLEN, sizeof(struct mmsghdr));
+    d->siov = calloc((size_t)d->nout * SEND_VLEN, sizeof(struct iovec));
+    d->stage = malloc((size_t)d->nout * SEND_VLEN * SR_DOWNSTREAM_BUF_SIZE);
+    d->nq = calloc((size_t)d->nout, sizeof(int));
+    d->alive = calloc((size_t)(c->downstream_num + 63) / 64, sizeof(uint64_t));
+    if (!d->sock_out || !d->smsg || !d->siov || !d->stage || !d->nq || !d->alive) {
+        sr_log(SR_ERROR, "%s: malloc() failed %s", fn, strerror(errno));
+        return thread_fail(d, 0);
+    }
+    for (int i = 0; i < d->nout; i++) {
+        if ((d->sock_out[i] = socket(AF_INET, SOCK_DGRAM, IPPROTO_UDP)) < 0) {
+            sr_log(SR_ERROR, "%s: socket_out socket() error %s", fn, strerror(errno));
+            return thread_fail(d, 0);
+        }
+    }
     d->alive_gen = (uint64_t)-1;
     refresh_alive(d);
     ev_io_init(&d->io, udp_read_cb, d->sock_in, EV_READ);
@@ -247,6 +285,22 @@ void *sr_data_thread(void *arg) {
     ev_run(d->loop, 0);
     sr_log(SR_ERROR, "%s: ev_loop() exited", fn);
     return NULL;
+}
+
+/* SIGHUP / SIGINT as the reference handles them (sr-init.c:177-185,290-297): a SIGHUP is logged and
+ * ignored (logrotate, init scripts), a SIGINT is logged and ends the process with status 0. Here they
+ * are libev signal watchers on the main thread's loop; the process exits without running the GPU
+ * runtime's teardown under the data threads. */
+static void on_sighup(struct ev_loop *loop, ev_signal *w, int revents) {
+    (void)loop, (void)w, (void)revents;
+    sr_log(SR_INFO, "%s: sighup received", "on_sighup");
+}
+
+static void on_sigint(struct ev_loop *loop, ev_signal *w, int revents) {
+    (void)loop, (void)w, (void)revents;
+    sr_log(SR_INFO, "%s: sigint received", "on_sigint");
+    fflush(stdout);
+    _exit(0);
 }
 
 int main(int argc, char *argv[]) {
@@ -268,6 +322,16 @@ int main(int argc, char *argv[]) {
 
     struct ev_loop *loop = ev_default_loop(0);
     const char *fn = "main";
+    static ev_signal sighup_w, sigint_w;
+    ev_signal_init(&sighup_w, on_sighup, SIGHUP);
+    ev_signal_start(loop, &sighup_w);
+    ev_signal_init(&sigint_w, on_sigint, SIGINT);
+    ev_signal_start(loop, &sigint_w);
+    /* a data thread whose GPU context cannot be opened ends the process (status 1) instead of leaving
+     * its share of the SO_REUSEPORT traffic unread; SR_REQUIRE_GPU=0 keeps the main thread's services
+     * (control port, health checks) running without data threads, for host-surface tests on CPU */
+    const char *rg = getenv("SR_REQUIRE_GPU");
+    config.require_gpu = !(rg && rg[0] == '0');
     int cs = socket(PF_INET, SOCK_STREAM, 0);
     if (cs < 0) {
         sr_log(SR_ERROR, "%s: socket() error %s", fn, strerror(errno));

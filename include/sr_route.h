@@ -325,11 +325,35 @@ int sr_pack_packets_many(sr_ctx *ctx, const sr_pack_batch *batches, size_t count
  * `fill` (n_downstreams u16) is the pending bytes per downstream before the batch and receives the
  * pending bytes after it; `sorted` (max_records) the regrouped records; `packets` (max_packets) the
  * descriptors; probed_dead (ceil(n/64) words, may be NULL) the dead downstreams whose pending
- * buffer the batch drops. Synchronous. Returns 0, -ENOSPC (records or descriptors did not fit:
- * outputs incomplete), -EINVAL, -ENOMEM, -EIO. */
+ * buffer the batch drops. Synchronous: one stream synchronisation (sr_route_pack_submit /
+ * sr_route_pack_result on a slot of its own). Returns 0, -ENOSPC (records or descriptors did not
+ * fit: outputs incomplete), -EINVAL, -ENOMEM, -EIO. */
 int sr_route_pack_batch(sr_ctx *ctx, const uint8_t *bytes, size_t nbytes, uint16_t *fill, sr_record *sorted,
                         size_t max_records, size_t *n_records, size_t *n_valid, sr_packet *packets,
                         size_t max_packets, size_t *n_packets, uint64_t *probed_dead);
+
+/* sr_route_pack_batch in two halves, for a data thread that overlaps a batch's GPU work with its own
+ * work on the previous batch (double buffering; reference: udp_read_cb, sr-main.c:149-191).
+ * sr_route_pack_submit enqueues on the context's stream the copy of `bytes` to the device, the route,
+ * the packing and one copy-out kernel that writes the batch's outputs (counts included) into
+ * page-locked memory the context owns for slot `slot` (0 or 1), and returns without waiting.
+ * fill: the pending bytes per downstream before the batch, or NULL to continue from the pending
+ * bytes the previous submission (of either slot, or sr_route_pack_batch) leaves on the device, all
+ * zero before the first: consecutive batches chain without a host round trip. `bytes` must stay
+ * unchanged until the slot's result is taken. sr_route_pack_result waits for the slot (its one
+ * synchronisation) and points *res at its outputs, valid until the slot is submitted again.
+ * A slot holds one batch at a time. Returns 0, -EBUSY (slot in use / not submitted), -ENOSPC
+ * (result: records or descriptors did not fit), -EINVAL, -ENOMEM, -EIO. */
+typedef struct sr_pack_result {
+    const sr_record *sorted;      /* n_records: valid lines by downstream, then the unrouted lines */
+    size_t n_records, n_valid;
+    const sr_packet *packets;     /* n_packets descriptors (sr_pack_packets)                       */
+    size_t n_packets;
+    const uint16_t *fill;         /* n_downstreams: pending bytes after the batch                  */
+    const uint64_t *probed_dead;  /* ceil(n_downstreams/64) words (sr-main.c:106)                  */
+} sr_pack_result;
+int sr_route_pack_submit(sr_ctx *ctx, int slot, const uint8_t *bytes, size_t nbytes, const uint16_t *fill);
+int sr_route_pack_result(sr_ctx *ctx, int slot, sr_pack_result *res);
 
 /* Page-locked host memory for the batches and outputs of the host-memory calls (their copies then
  * run at full link rate). NULL on failure. */

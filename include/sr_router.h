@@ -64,12 +64,28 @@ int sr_core_open(sr_core **core, const sr_core_config *cfg, sr_core_emit_fn emit
  * reference (sr-init.c:85). */
 int sr_core_set_alive(sr_core *core, const uint64_t *alive);
 
-/* A page-locked buffer of max_batch_bytes the caller may frame datagrams into (optional). */
+/* A page-locked buffer of max_batch_bytes the caller may frame datagrams into (optional; it is slot
+ * 0's buffer of the double-buffered calls below). */
 uint8_t *sr_core_batch_buffer(sr_core *core, size_t *capacity);
 
 /* Route one batch of framed datagrams (sr_frame_datagram output, back to back): what the
  * reference does in udp_read_cb for each datagram in turn (sr-main.c:149-191). */
 int sr_core_route(sr_core *core, const uint8_t *framed, size_t nbytes);
+
+/* Double-buffered routing: the host's work on one batch (walking its packets, the emit and log
+ * callbacks, receiving the next datagrams) overlaps the GPU's work on the next (sr_route_pack_submit).
+ * The core owns two page-locked batch buffers, slots 0 and 1 (sr_core_slot_buffer). sr_core_submit
+ * starts routing slot `slot`'s first nbytes, then completes the OTHER slot's batch if one is in
+ * flight (its packets are emitted, its WARN lines logged, the flush callback called), so when it
+ * returns at most `slot` is in flight and the other slot's buffer may be refilled. sr_core_drain
+ * completes the batch in flight, if any. Batches complete in submission order, with exactly the
+ * packets, pending buffers, counters and log lines that sr_core_route would produce for them one
+ * after another; pending bytes chain on the device between batches. sr_core_route,
+ * sr_core_flush_timer, sr_core_ping and sr_core_set_alive drain first. Returns 0, -EBUSY (the slot is
+ * in flight), -EINVAL or an sr_route_pack_* error. */
+uint8_t *sr_core_slot_buffer(sr_core *core, int slot, size_t *capacity);
+int sr_core_submit(sr_core *core, int slot, size_t nbytes);
+int sr_core_drain(sr_core *core);
 
 /* ds_flush_timer_cb (sr-main.c:194-204): flush every non-empty pending buffer. */
 int sr_core_flush_timer(sr_core *core);

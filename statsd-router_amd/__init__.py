@@ -51,7 +51,7 @@ ABI_FUNCTIONS = (
     "sr_route_batch", "sr_last_probed_dead", "sr_route_device", "sr_route_device_many", "sr_pack_by_owner",
     "sr_pack_many_by_owner", "sr_pack_packets", "sr_pack_packets_many", "sr_route_pack_batch", "sr_alloc_host", "sr_free_host", "sr_sync", "sr_close", "sr_version",
     "sr_comm_id", "sr_comm_open", "sr_comm_close", "sr_exchange_sizes", "sr_exchange_data",
-    "sr_exchange_plan", "sr_exchange_run", "sr_exchange_rebase",
+    "sr_exchange_plan", "sr_exchange_run", "sr_exchange_rebase", "sr_route_pack_submit", "sr_route_pack_result",
 )
 SR_MAX_PACK_DOWNSTREAMS = 4096
 SR_LAYOUT_AUTO, SR_LAYOUT_UNIFORM, SR_LAYOUT_SEGMENTS = 0, 1, 2
@@ -91,6 +91,13 @@ class SrPackBatch(ctypes.Structure):
         ("d_packets", ctypes.c_void_p), ("max_packets", ctypes.c_size_t), ("d_counts", ctypes.c_void_p),
         ("d_fill_out", ctypes.c_void_p),
     ]
+
+
+class SrPackResult(ctypes.Structure):
+    """struct sr_pack_result (include/sr_route.h): the outputs of a sr_route_pack_submit slot."""
+    _fields_ = [("sorted", ctypes.c_void_p), ("n_records", ctypes.c_size_t), ("n_valid", ctypes.c_size_t),
+                ("packets", ctypes.c_void_p), ("n_packets", ctypes.c_size_t), ("fill", ctypes.c_void_p),
+                ("probed_dead", ctypes.c_void_p)]
 
 
 class SrExchangePeer(ctypes.Structure):
@@ -185,6 +192,8 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_exchange_run": (ctypes.c_int, [ctypes.POINTER(SrTransport), ctypes.c_int, ctypes.c_int, vp, vp, vp, vp,
                                            vp, vp]),
         "sr_exchange_rebase": (ctypes.c_int, [vp, vp, vp, ctypes.c_int]),
+        "sr_route_pack_submit": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_size_t, vp]),
+        "sr_route_pack_result": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(SrPackResult)]),
     }
     for name in ABI_FUNCTIONS:
         fn = getattr(lib, name)  # raises AttributeError if the export is missing
@@ -401,6 +410,35 @@ class Router:
                                              pk.ctypes.data, mp, ctypes.byref(npk), pw.ctypes.data),
                "sr_route_pack_batch")
         return srt[: nr.value], pk[: npk.value], f[:n].copy(), nv.value, bitmap_shards(pw, n)
+
+    def route_pack_submit(self, slot: int, data, fill=None) -> None:
+        """sr_route_pack_submit (asynchronous). data must stay alive and unchanged until
+        route_pack_result(slot): keep a reference (e.g. a pinned or numpy buffer). fill None = chain
+        from the previous submission's pending bytes on the device."""
+        buf = np.frombuffer(data, dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else np.ascontiguousarray(data, dtype=np.uint8)
+        f = None
+        if fill is not None:
+            f = np.zeros(max(self.n_downstreams, 1), dtype=np.uint16)
+            f[: self.n_downstreams] = np.asarray(fill, dtype=np.uint16)
+        self._pending = getattr(self, "_pending", {})
+        self._pending[slot] = buf
+        _check(self._lib.sr_route_pack_submit(self._h, slot, buf.ctypes.data if buf.size else None, int(buf.size),
+                                              f.ctypes.data if f is not None else None), "sr_route_pack_submit")
+
+    def route_pack_result(self, slot: int):
+        """sr_route_pack_result: (sorted records, packets, fill after, n_valid, probed-dead shard ids),
+        copied out of the slot."""
+        r = SrPackResult()
+        _check(self._lib.sr_route_pack_result(self._h, slot, ctypes.byref(r)), "sr_route_pack_result")
+        n = self.n_downstreams
+        take = lambda addr, count, dt: (np.frombuffer((ctypes.c_uint8 * (count * dt.itemsize)).from_address(addr),
+                                                      dtype=dt).copy() if count else np.zeros(0, dt))
+        srt = take(r.sorted, r.n_records, RECORD_DTYPE)
+        pk = take(r.packets, r.n_packets, PACKET_DTYPE)
+        fill = take(r.fill, n, np.dtype(np.uint16))
+        pw = take(r.probed_dead, max((n + 63) // 64, 1), np.dtype(np.uint64))
+        getattr(self, "_pending", {}).pop(slot, None)
+        return srt, pk, fill, int(r.n_valid), bitmap_shards(pw, n)
 
     def pack_packets(self, d_recs: int, d_n_records: int, max_records: int, d_fill_in: int | None,
                      d_probed_dead: int | None, d_sorted: int, d_packets: int, max_pk: int, d_counts: int,

@@ -48,6 +48,10 @@ def router_lib() -> ctypes.CDLL:
         L.sr_core_batch_buffer.restype = vp
         L.sr_core_batch_buffer.argtypes = [vp, ctypes.POINTER(ctypes.c_size_t)]
         L.sr_core_route.restype, L.sr_core_route.argtypes = ctypes.c_int, [vp, vp, ctypes.c_size_t]
+        L.sr_core_slot_buffer.restype = vp
+        L.sr_core_slot_buffer.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
+        L.sr_core_submit.restype, L.sr_core_submit.argtypes = ctypes.c_int, [vp, ctypes.c_int, ctypes.c_size_t]
+        L.sr_core_drain.restype, L.sr_core_drain.argtypes = ctypes.c_int, [vp]
         L.sr_core_flush_timer.restype, L.sr_core_flush_timer.argtypes = ctypes.c_int, [vp]
         L.sr_core_ping.restype, L.sr_core_ping.argtypes = ctypes.c_int, [vp]
         L.sr_core_state.restype = ctypes.c_int
@@ -120,6 +124,21 @@ class Core:
             raise SrError(28, "batch larger than the core's buffer")
         ctypes.memmove(p, bytes(framed), len(framed))
         _check(self._L.sr_core_route(self._h, p, len(framed)), "sr_core_route")
+
+    def submit(self, framed: bytes) -> None:
+        """Double-buffered: frame into the next slot's buffer and sr_core_submit it (the previous
+        batch completes here, the new one stays in flight until the next submit or drain)."""
+        slot = getattr(self, "_slot", 0)
+        cap = ctypes.c_size_t()
+        p = self._L.sr_core_slot_buffer(self._h, slot, ctypes.byref(cap))
+        if len(framed) > cap.value:
+            raise SrError(28, "batch larger than the core's buffer")
+        ctypes.memmove(p, bytes(framed), len(framed))
+        _check(self._L.sr_core_submit(self._h, slot, len(framed)), "sr_core_submit")
+        self._slot = slot ^ 1
+
+    def drain(self) -> None:
+        _check(self._L.sr_core_drain(self._h), "sr_core_drain")
 
     def flush_timer(self) -> None:
         _check(self._L.sr_core_flush_timer(self._h), "sr_core_flush_timer")

@@ -666,3 +666,41 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuLaunch L) {
 }
 
 }  // namespace srk
+
+namespace srk {
+
+// The outputs of one routed + packed batch copied into page-locked host memory (device-mapped) by
+// one kernel on the batch's stream, so that a host waits once per batch (sr_route_pack_result):
+// the copy sizes are the device's own counts, which no host round trip has to fetch first.
+struct PackOut {
+    const sr_record *sorted;
+    const sr_packet *packets;
+    const uint16_t *fill;        // pending bytes after the batch (n_downstreams)
+    const uint64_t *probed;      // null: no dead shard in the snapshot (zeros written)
+    const uint64_t *counts;      // {descriptors, valid lines, lines}
+    uint64_t rec_cap, pk_cap;
+    uint32_t nds, nwords;
+    sr_record *h_sorted;         // device-mapped host pointers
+    sr_packet *h_packets;
+    uint16_t *h_fill;
+    uint64_t *h_probed;
+    uint64_t *h_counts;
+};
+
+__global__ __launch_bounds__(256) void pack_out_kernel(PackOut o) {
+    const uint64_t np = min(o.counts[0], o.pk_cap), nr = min(o.counts[2], o.rec_cap);
+    const uint64_t tid = (uint64_t)blockIdx.x * 256u + threadIdx.x, stride = (uint64_t)gridDim.x * 256u;
+    // records as 16-byte pairs (the tail record alone), packets 16 bytes each
+    const uint4 *rs = reinterpret_cast<const uint4 *>(o.sorted);
+    uint4 *rd = reinterpret_cast<uint4 *>(o.h_sorted);
+    for (uint64_t i = tid; i < nr / 2; i += stride) rd[i] = rs[i];
+    if ((nr & 1) && tid == 0) o.h_sorted[nr - 1] = o.sorted[nr - 1];
+    const uint4 *ps = reinterpret_cast<const uint4 *>(o.packets);
+    uint4 *pd = reinterpret_cast<uint4 *>(o.h_packets);
+    for (uint64_t i = tid; i < np; i += stride) pd[i] = ps[i];
+    for (uint64_t i = tid; i < o.nds; i += stride) o.h_fill[i] = o.fill[i];
+    for (uint64_t i = tid; i < o.nwords; i += stride) o.h_probed[i] = o.probed ? o.probed[i] : 0ull;
+    if (tid < 3) o.h_counts[tid] = o.counts[tid];
+}
+
+}  // namespace srk

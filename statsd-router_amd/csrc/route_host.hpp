@@ -7,11 +7,27 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
+#include <utility>
 #include <vector>
 
 #include "route_kernel.hpp"
 
 namespace srk {
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (device, kernel) of the process: data
+// threads of one executable may run contexts on several devices at once.
+inline void ensure_dyn_lds(const void *fn, int bytes) {
+    static std::mutex mu;
+    static std::vector<std::pair<int, const void *>> done;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    std::lock_guard<std::mutex> g(mu);
+    for (const auto &e : done)
+        if (e.first == dev && e.second == fn) return;
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    done.emplace_back(dev, fn);
+}
 
 inline Magic make_magic(uint64_t d) {
     Magic mg{0, 0, 0};
@@ -256,7 +272,7 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
     }
     RouteParams p = in;
     p.nb = 0;
-    uint64_t replay_blocks = 0;   // probed_dead_kernel blocks (batches that asked for the bitmap)
+    bool replay = false;   // some batch asked for the probed-dead bitmap (probed_dead_kernel)
     for (uint32_t i = 0; i < in.nb; ++i) {
         // the probed-dead bitmap starts empty; with every shard alive nothing can set it
         if (in.b[i].probed_dead) {
@@ -272,7 +288,7 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
         }
         p.b[p.nb++] = in.b[i];
         if (ds.dead == 0) p.b[p.nb - 1].probed_dead = nullptr;
-        if (p.b[p.nb - 1].probed_dead) replay_blocks += (p.b[p.nb - 1].max_records + 255u) / 256u;
+        if (p.b[p.nb - 1].probed_dead) replay = true;
     }
     if (p.nb == 0) return 0;
     // 8+ batches: each batch's tiles on one XCD class; its scanner (block j) shares that class
@@ -311,18 +327,13 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
     hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     if (hipGetLastError() != hipSuccess) return -EIO;
     if (ds.wide()) {
-        static bool attr_set = false;
-        if (!attr_set) {
-            (void)hipFuncSetAttribute((const void *)probe_wide_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024);
-            attr_set = true;
-        }
+        ensure_dyn_lds((const void *)probe_wide_kernel, 160 * 1024);
         hipLaunchKernelGGL(probe_wide_kernel, dim3(256), dim3(64), (size_t)ds.nds * sizeof(uint16_t), stream, p);
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
-    if (replay_blocks) {   // dead shards and a bitmap asked for: replay the probes (sr-main.c:106)
-        if (replay_blocks > 0x7FFFFFFFull) return -EINVAL;
-        hipLaunchKernelGGL(probed_dead_kernel, dim3((uint32_t)replay_blocks), dim3(256), 0, stream, p);
+    if (replay) {   // dead shards and a bitmap asked for: replay the probes (sr-main.c:106)
+        p.nwords_check = ds.nwords <= kReplayCheckWords ? ds.nwords : 0u;
+        hipLaunchKernelGGL(probed_dead_kernel, dim3(kReplayBlocks, p.nb), dim3(256), 0, stream, p);
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
     return 0;

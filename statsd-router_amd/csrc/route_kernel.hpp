@@ -11,31 +11,38 @@
 // (host framing, sr_frame_datagram), so the lines of the batch are its '\n'-terminated pieces and
 // datagram boundaries are irrelevant here. Output: one 8-byte sr_record per line, in input order.
 //
-// One kernel, one pass over the bytes (DESIGN.md §3):
-//   * 64 KiB tiles, tile = blockIdx.x, one 1024-thread workgroup each (one per CU).
-//   * Tile bytes: coalesced 1 KiB-per-wave-instruction buffer loads -> LDS; each lane then owns
-//     64 contiguous bytes.
-//   * Per lane: '\n' and ':' bitmasks (SWAR) and the unmasked sdbm Horner value of its 64 bytes.
-//     The name hash of a line [s, c) is a difference of Horner prefixes,
-//         h = P(c-1) - P(s-1) * K^(c-s)   (mod 2^64, K = 65599),
-//     P over the tile comes from a wave + workgroup scan of the lane values (multiplier K^64) and
-//     is stored per 16-byte piece in LDS.
-//   * Line numbering: a workgroup scan of per-lane '\n' counts gives tile-local line indices; the
-//     tile's first record index comes from a decoupled look-back over per-tile counts (8-byte
-//     {epoch, flag, count} granules written and polled with agent-scope relaxed atomics: the data
-//     is the flag). A tile publishes its count straight after its loads; one wave polls up to
-//     1024 predecessors per round while the other waves stage their lines. A predecessor that has
-//     not published within a bounded spin is counted by the waiting wave itself, so progress
-//     never depends on dispatch order.
-//   * The line that straddles into the tile (at most one) is finished by the last wave from the
-//     1 KiB before the tile, loaded at kernel start (further windows only for lines > 1 KiB).
-//   * Shard pick: h % N through a 64-bit magic reciprocal when every shard is alive; otherwise
-//     the reference's probe with a 16-entry register overlay of the permutation (each dead shard
-//     is probed at most once per line). Lines needing more than 16 dead probes are deferred to
-//     probe_wide_kernel (the probe on a full LDS permutation).
-//   * Every workgroup arrives on 8-way sharded counters without waiting; the last tile waits for
-//     all arrivals and advances the context's epoch, so stale look-back granules of earlier
-//     launches are never mistaken for current ones, with or without graph replay.
+// One kernel, one pass over the bytes (DESIGN.md §5.1):
+//   * A launch routes up to 32 batches. Blocks 0 .. nb-1 are per-batch SCANNERS; every other block
+//     routes one 16 KiB TILE with 256 threads (4 waves), 64 contiguous bytes per thread, up to 7
+//     workgroups per CU (71-72 VGPRs, ~22.5 KiB of LDS). With 8+ batches each batch's tiles and its
+//     scanner share one XCD class (blocks b and b + 8 land on the same XCD).
+//   * Tile entry: four buffer_load_dwordx4 per thread (+ 2 KiB of halo before the tile) into a padded
+//     LDS image (17-dword rows: conflict-free per-thread rows); '\n' and ':' bit masks of the
+//     thread's 64 bytes from the load registers (8 VALU per dword for both patterns); the tile's '\n'
+//     count published at once in a status granule for the scanner.
+//   * Record numbering: the scanner polls its batch's tile counts (two polls in flight, 64 tiles per
+//     poll) and publishes each tile's first record index (bases granule: plain store when the tile
+//     shares the scanner's XCD, sc1 otherwise); a second scanner wave does the stores. A tile reads
+//     its base part-way through its hashing, long after it is normally published; a tile that never
+//     published within a spin budget is counted by the scanner itself (no dispatch-order assumption).
+//   * Line state per thread (lines before its chunk, first ':' of the line open at its start) from
+//     two u32 DPP wave scans plus the earlier waves' totals; the line straddling into the tile (at
+//     most one) is located in the halo (or in global memory for lines longer than it).
+//   * Lines, in windows of 256 tile-local lines: (end, first ':') staged in LDS, then every line
+//     hashed from the LDS image: sdbm with SDWA byte-pair products and one 64x64 multiply per 8
+//     bytes (sdbm_img), a name of n bytes being ceil(n/64) 64-byte segments combined with K^len.
+//     Two lane layouts, one instantiation each (identical records): KV_UNIFORM gives every line of
+//     a tile the same G lanes (from the tile's mean line length); KV_SEGMENTS gives a tile of mixed
+//     lengths one lane per segment, lines packed back to back over the lanes, a line's hash the
+//     difference of an inclusive wave scan of segment hashes (route_host.hpp picks per launch).
+//   * Shard pick: h % N through a 64-bit magic reciprocal when every shard is alive; otherwise the
+//     reference's probe with a 16-entry register overlay of the permutation (the first reciprocals
+//     in LDS). Lines needing more than 16 dead probes are deferred to probe_wide_kernel (the probe
+//     on a full LDS permutation); the dead shards the probes visit (sr-main.c:106) come from
+//     probed_dead_kernel, a replay after the launch.
+//   * Every workgroup arrives on 8-way sharded counters without waiting; the last block waits for
+//     all arrivals and advances the context's epoch, so stale granules of earlier launches are never
+//     mistaken for current ones, with or without graph replay.
 // No MFMA: HBM-bound byte work on VALU + LDS.
 #pragma once
 
@@ -160,6 +167,8 @@ struct RouteParams {
     uint32_t nds;            // number of downstreams
     uint32_t dead;           // dead downstreams in the alive snapshot
     uint32_t pending_cap;
+    uint32_t nwords_check;   // probed_dead_kernel: bitmap words checked for completion (0: never)
+    uint32_t pad_nw;
     Magic magic_n;           // for h % nds (fast path)
     const uint64_t *alive;   // bitmap
     const Magic *magic;      // [0..nds], index i -> divisor i
@@ -1744,50 +1753,65 @@ __global__ __launch_bounds__(64) void probe_wide_kernel(RouteParams p) {
 }
 
 // The dead-downstream side effect (sr-main.c:106), replayed after a launch when some shards are
-// dead and a batch asked for its probed-dead bitmap: one lane per record, the name's sdbm
-// recomputed from the batch bytes (aligned dword loads, the first ':' ends it), then the probe of
-// find_downstream with every dead shard it visits set in the bitmap. Lines that needed more than
-// kOverlay dead probes were resolved by probe_wide_kernel, which sets their bits itself.
-__global__ __launch_bounds__(256) void probed_dead_kernel(RouteParams p) {
-    // the batch of this block: batches in order, ceil(max_records / 256) blocks each
-    uint32_t bi = 0, blk = blockIdx.x;
-    for (; bi < p.nb; ++bi) {
-        const uint32_t nbk = (p.b[bi].max_records + 255u) / 256u;
-        if (blk < nbk) break;
-        blk -= nbk;
+// dead and a batch asked for its probed-dead bitmap: per record, the name's sdbm recomputed from the
+// batch bytes (aligned dword loads, the first ':' ends it), then the probe of find_downstream with
+// every dead shard it visits set in the bitmap. Lines that needed more than kOverlay dead probes were
+// resolved by probe_wide_kernel, which sets their bits itself.
+// The bitmap can only ever hold the snapshot's dead shards, and in a large batch every one of them is
+// some line's first pick within the first few thousand lines: kReplayBlocks workgroups per batch
+// (grid y = batch) stride over its records and stop as soon as the bitmap holds every dead shard
+// (checked per stride, a few L2 reads), so the replay re-hashes a few thousand lines, not the batch.
+constexpr uint32_t kReplayBlocks = 32;
+constexpr uint32_t kReplayCheckWords = 16;   // bitmaps up to 1024 shards are checked for completion
+
+__device__ __forceinline__ bool all_dead_noted(const RouteParams &p, const uint64_t *pd) {
+    if (p.nwords_check == 0) return false;
+    for (uint32_t w = 0; w < p.nwords_check; ++w) {
+        const uint32_t hi = p.nds - 64 * w;
+        const uint64_t full = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+        const uint64_t seen = __hip_atomic_load(pd + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | p.alive[w];
+        if ((seen & full) != full) return false;
     }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void probed_dead_kernel(RouteParams p) {
+    const uint32_t bi = blockIdx.y;
     if (bi >= p.nb) return;
     const BatchDesc &bd = p.b[bi];
     if (!bd.probed_dead) return;
     const uint32_t n = (uint32_t)min(*bd.n_out, (uint64_t)bd.max_records);
-    const uint32_t i = blk * 256u + threadIdx.x;
-    if (i >= n) return;
-    const sr_record r = bd.recs[i];
-    if (r.route == SR_ROUTE_INVALID_LENGTH || r.route == SR_ROUTE_INVALID_FORMAT) return;
-    if (r.route == SR_ROUTE_ALL_DEAD) {   // every shard dead: the probe visited all of them
-        if (p.dead >= p.nds && p.nds) note_all_dead(bd.probed_dead, p.nds);
-        return;
-    }
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
-    // sdbm over the bytes before the first ':' (sr-main.c:120-134); the record is valid, so a ':'
-    // lies within the line
-    uint64_t h = 0;
-    const uint32_t a0 = r.offset & ~3u, end = r.offset + r.length;
-    bool done = false;
-    for (uint32_t a = a0; a < end && !done; a += 4) {
-        const uint32_t x = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a, 0, 0);
+    for (uint32_t i0 = blockIdx.x * 256u; i0 < n; i0 += gridDim.x * 256u) {
+        if (all_dead_noted(p, bd.probed_dead)) return;   // the same answer for every lane
+        const uint32_t i = i0 + threadIdx.x;
+        if (i >= n) continue;
+        const sr_record r = bd.recs[i];
+        if (r.route == SR_ROUTE_INVALID_LENGTH || r.route == SR_ROUTE_INVALID_FORMAT) continue;
+        if (r.route == SR_ROUTE_ALL_DEAD) {   // every shard dead: the probe visited all of them
+            if (p.dead >= p.nds && p.nds) note_all_dead(bd.probed_dead, p.nds);
+            continue;
+        }
+        // sdbm over the bytes before the first ':' (sr-main.c:120-134); the record is valid, so a
+        // ':' lies within the line
+        uint64_t h = 0;
+        const uint32_t a0 = r.offset & ~3u, end = r.offset + r.length;
+        bool done = false;
+        for (uint32_t a = a0; a < end && !done; a += 4) {
+            const uint32_t x = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a, 0, 0);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t pos = a + (uint32_t)q;
-            const uint32_t c = (x >> (8 * q)) & 0xFFu;
-            if (!done && pos >= r.offset && pos < end) {
-                if (c == (uint32_t)':') done = true;
-                else h = sdbm_step(h, c);
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t pos = a + (uint32_t)q;
+                const uint32_t c = (x >> (8 * q)) & 0xFFu;
+                if (!done && pos >= r.offset && pos < end) {
+                    if (c == (uint32_t)':') done = true;
+                    else h = sdbm_step(h, c);
+                }
             }
         }
+        (void)probe_shard<true>(h, p, bd.probed_dead);
     }
-    (void)probe_shard<true>(h, p, bd.probed_dead);
 }
 
 }  // namespace srk

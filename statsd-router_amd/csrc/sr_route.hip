@@ -49,8 +49,22 @@ struct sr_ctx {
     size_t d_sorted_cap;
     sr_packet *d_packets;
     size_t d_packets_cap;
-    uint16_t *d_fill;             // [2][nds]: in, out
+    uint16_t *d_fill;             // [3][nds]: two chained outputs, then the uploaded fill of a submission
+    int fill_cur;                 // region of d_fill holding the last submission's output (0 or 1)
     uint64_t *d_mcounts;          // 3 u64
+    // page-locked, device-mapped outputs of sr_route_pack_submit: slots 0 and 1, slot 2 is
+    // sr_route_pack_batch's own
+    struct Slot {
+        uint8_t *host;            // one allocation: records | packets | fill out | probed | counts | fill in
+        uint8_t *dev;             // its device-mapped address
+        size_t rec_cap, pk_cap;
+        hipEvent_t done;
+        int busy;                 // submitted, result not taken
+        sr_record *sorted;
+        sr_packet *packets;
+        uint16_t *fill, *fill_in;
+        uint64_t *probed, *counts;
+    } slot[3];
 };
 
 static void free_ptr(void *p) { (void)hipFree(p); }
@@ -146,6 +160,10 @@ void sr_close(sr_ctx *c) {
     free_ptr(c->d_packets);
     free_ptr(c->d_fill);
     free_ptr(c->d_mcounts);
+    for (auto &sl : c->slot) {
+        if (sl.host) (void)hipHostFree(sl.host);
+        if (sl.done) (void)hipEventDestroy(sl.done);
+    }
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
     free(c);
 }
@@ -427,14 +445,9 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     L.dbg = nullptr;
 #endif
     const size_t sort_lds = (size_t)kMtuSortWaves * (nds + 1) * sizeof(uint32_t);
-    static bool sort_attr = false;   // up to 4 x 4097 counters: past the 64 KiB default
-    if (!sort_attr) {
-        (void)hipFuncSetAttribute((const void *)mtu_count_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  96 * 1024);
-        (void)hipFuncSetAttribute((const void *)mtu_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  96 * 1024);
-        sort_attr = true;
-    }
+    // up to 4 x 4097 counters: past the 64 KiB default
+    ensure_dyn_lds((const void *)mtu_count_kernel, 96 * 1024);
+    ensure_dyn_lds((const void *)mtu_scatter_kernel, 96 * 1024);
     const uint32_t sort_blocks = (tiles + kMtuSortWaves - 1) / kMtuSortWaves;
     hipLaunchKernelGGL(mtu_count_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
     hipLaunchKernelGGL(mtu_scan_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
@@ -469,6 +482,140 @@ static int grow(void **ptr, size_t *cap, size_t need, size_t elem) {
     return 0;
 }
 
+// Host outputs of a slot for batches of up to nbytes (grown, never shrunk; the slot is idle).
+static size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
+static int slot_reserve(sr_ctx *c, int k, size_t nbytes) {
+    sr_ctx::Slot &sl = c->slot[k];
+    const size_t nds = c->ds.nds, nw = c->ds.nwords ? c->ds.nwords : 1;
+    const size_t rec = nbytes, pk = (size_t)SR_MAX_PACKETS(nbytes, c->ds.nds);
+    if (!sl.done && hipEventCreateWithFlags(&sl.done, hipEventDisableTiming) != hipSuccess) {
+        sl.done = nullptr;
+        return -ENOMEM;
+    }
+    if (sl.host && rec <= sl.rec_cap && pk <= sl.pk_cap) return 0;
+    if (sl.host) (void)hipHostFree(sl.host);
+    sl.host = sl.dev = nullptr;
+    sl.rec_cap = sl.pk_cap = 0;
+    const size_t o_pk = up256(rec * sizeof(sr_record)), o_fill = o_pk + up256(pk * sizeof(sr_packet));
+    const size_t o_pr = o_fill + up256(nds * sizeof(uint16_t) + 2), o_cnt = o_pr + up256(nw * sizeof(uint64_t));
+    const size_t o_fin = o_cnt + 256, total = o_fin + up256(nds * sizeof(uint16_t) + 2);
+    void *h = nullptr;
+    if (hipHostMalloc(&h, total, hipHostMallocMapped) != hipSuccess) return -ENOMEM;
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        (void)hipHostFree(h);
+        return -EIO;
+    }
+    sl.host = (uint8_t *)h;
+    sl.dev = (uint8_t *)d;
+    sl.rec_cap = rec;
+    sl.pk_cap = pk;
+    sl.sorted = (sr_record *)sl.host;
+    sl.packets = (sr_packet *)(sl.host + o_pk);
+    sl.fill = (uint16_t *)(sl.host + o_fill);
+    sl.probed = (uint64_t *)(sl.host + o_pr);
+    sl.counts = (uint64_t *)(sl.host + o_cnt);
+    sl.fill_in = (uint16_t *)(sl.host + o_fin);
+    return 0;
+}
+
+static int pack_submit(sr_ctx *c, int k, const uint8_t *bytes, size_t nbytes, const uint16_t *fill) {
+    sr_ctx::Slot &sl = c->slot[k];
+    if (sl.busy) return -EBUSY;
+    if ((nbytes && !bytes) || nbytes > c->ds.max_batch) return -EINVAL;
+    if (c->ds.nds > SR_MAX_PACK_DOWNSTREAMS) return -EINVAL;
+    if (nbytes && bytes[nbytes - 1] != '\n') return -EINVAL;
+    (void)hipSetDevice(c->device);
+    const size_t nds = c->ds.nds, nw = c->ds.nwords;
+    int rc;
+    if ((rc = slot_reserve(c, k, nbytes ? nbytes : 1))) return rc;
+    const size_t cap = nbytes ? nbytes : 1;   // never more lines than bytes
+    const size_t pcap = (size_t)SR_MAX_PACKETS(cap, nds);
+    if ((rc = grow((void **)&c->d_out, &c->d_out_cap, cap, sizeof(sr_record)))) return rc;
+    if ((rc = grow((void **)&c->d_sorted, &c->d_sorted_cap, cap, sizeof(sr_record)))) return rc;
+    if ((rc = grow((void **)&c->d_packets, &c->d_packets_cap, pcap, sizeof(sr_packet)))) return rc;
+    if (!c->d_fill) {
+        if (hipMalloc(&c->d_fill, (3 * nds + 2) * sizeof(uint16_t)) != hipSuccess) {
+            c->d_fill = nullptr;
+            return -ENOMEM;
+        }
+        if (hipMemsetAsync(c->d_fill, 0, (3 * nds + 2) * sizeof(uint16_t), c->stream) != hipSuccess) return -EIO;
+        c->fill_cur = 0;
+    }
+    if (!c->d_mcounts && hipMalloc(&c->d_mcounts, 4 * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+    uint16_t *const f_in = fill ? c->d_fill + 2 * nds : c->d_fill + (size_t)c->fill_cur * nds;
+    uint16_t *const f_out = c->d_fill + (size_t)(c->fill_cur ^ 1) * nds;
+    if (fill && nds) {   // staged in the slot's page-locked memory: the caller's array is free on return
+        memcpy(sl.fill_in, fill, nds * sizeof(uint16_t));
+        if (hipMemcpyAsync(f_in, sl.fill_in, nds * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+            return -EIO;
+    }
+    if (nbytes == 0) {   // no lines: the fills carry over, nothing is probed
+        if (nds && hipMemcpyAsync(f_out, f_in, nds * sizeof(uint16_t), hipMemcpyDeviceToDevice, c->stream) != hipSuccess)
+            return -EIO;
+        if (hipMemsetAsync(c->d_mcounts, 0, 4 * sizeof(uint64_t), c->stream) != hipSuccess) return -EIO;
+    } else {
+        if (hipMemcpyAsync(c->d_in, bytes, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return -EIO;
+        RouteParams p = c->ds.params();
+        DeviceState::add_batch(p, c->d_in, nbytes, c->d_out, cap, nullptr, c->d_count, c->d_probed);
+        if ((rc = launch_variant(c->ds, p, c->stream))) return rc;
+        if ((rc = sr_pack_packets(c, c->d_out, c->d_count, cap, f_in, c->ds.dead ? c->d_probed : nullptr,
+                                  c->d_sorted, c->d_packets, pcap, c->d_mcounts, f_out)))
+            return rc;
+    }
+    c->fill_cur ^= 1;
+    PackOut o;
+    o.sorted = c->d_sorted;
+    o.packets = c->d_packets;
+    o.fill = f_out;
+    o.probed = (nbytes && c->ds.dead) ? c->d_probed : nullptr;
+    o.counts = c->d_mcounts;
+    o.rec_cap = sl.rec_cap;
+    o.pk_cap = sl.pk_cap;
+    o.nds = (uint32_t)nds;
+    o.nwords = (uint32_t)nw;
+    o.h_sorted = (sr_record *)(sl.dev + ((uint8_t *)sl.sorted - sl.host));
+    o.h_packets = (sr_packet *)(sl.dev + ((uint8_t *)sl.packets - sl.host));
+    o.h_fill = (uint16_t *)(sl.dev + ((uint8_t *)sl.fill - sl.host));
+    o.h_probed = (uint64_t *)(sl.dev + ((uint8_t *)sl.probed - sl.host));
+    o.h_counts = (uint64_t *)(sl.dev + ((uint8_t *)sl.counts - sl.host));
+    // one workgroup per 512 records (two per thread), at most 1024 workgroups (grid-stride beyond)
+    const uint64_t want = (cap + 511) / 512;
+    hipLaunchKernelGGL(pack_out_kernel, dim3((uint32_t)(want < 1024 ? (want ? want : 1) : 1024)), dim3(256), 0,
+                       c->stream, o);
+    if (hipGetLastError() != hipSuccess) return -EIO;
+    if (hipEventRecord(sl.done, c->stream) != hipSuccess) return -EIO;
+    sl.busy = 1;
+    return 0;
+}
+
+static int pack_result(sr_ctx *c, int k, sr_pack_result *res) {
+    sr_ctx::Slot &sl = c->slot[k];
+    if (!sl.busy) return -EBUSY;
+    sl.busy = 0;
+    (void)hipSetDevice(c->device);
+    if (hipEventSynchronize(sl.done) != hipSuccess) return -EIO;
+    const uint64_t np = sl.counts[0], nv = sl.counts[1], nr = sl.counts[2];
+    res->sorted = sl.sorted;
+    res->packets = sl.packets;
+    res->fill = sl.fill;
+    res->probed_dead = sl.probed;
+    res->n_records = (size_t)(nr < sl.rec_cap ? nr : sl.rec_cap);
+    res->n_valid = (size_t)(nv < res->n_records ? nv : res->n_records);
+    res->n_packets = (size_t)(np < sl.pk_cap ? np : sl.pk_cap);
+    return (nr > sl.rec_cap || np > sl.pk_cap) ? -ENOSPC : 0;
+}
+
+int sr_route_pack_submit(sr_ctx *c, int slot, const uint8_t *bytes, size_t nbytes, const uint16_t *fill) {
+    if (!c || slot < 0 || slot > 1) return -EINVAL;
+    return pack_submit(c, slot, bytes, nbytes, fill);
+}
+
+int sr_route_pack_result(sr_ctx *c, int slot, sr_pack_result *res) {
+    if (!c || !res || slot < 0 || slot > 1) return -EINVAL;
+    return pack_result(c, slot, res);
+}
+
 int sr_route_pack_batch(sr_ctx *c, const uint8_t *bytes, size_t nbytes, uint16_t *fill, sr_record *sorted,
                         size_t max_records, size_t *n_records, size_t *n_valid, sr_packet *packets,
                         size_t max_packets, size_t *n_packets, uint64_t *probed_dead) {
@@ -481,52 +628,21 @@ int sr_route_pack_batch(sr_ctx *c, const uint8_t *bytes, size_t nbytes, uint16_t
         if (probed_dead && nw) memset(probed_dead, 0, nw * sizeof(uint64_t));
         return 0;
     }
-    if (bytes[nbytes - 1] != '\n') return -EINVAL;
-    (void)hipSetDevice(c->device);
-    const size_t cap = nbytes;   // never more lines than bytes
-    const size_t pcap = (size_t)SR_MAX_PACKETS(nbytes, c->ds.nds);
-    int rc;
-    if ((rc = grow((void **)&c->d_out, &c->d_out_cap, cap, sizeof(sr_record)))) return rc;
-    if ((rc = grow((void **)&c->d_sorted, &c->d_sorted_cap, cap, sizeof(sr_record)))) return rc;
-    if ((rc = grow((void **)&c->d_packets, &c->d_packets_cap, pcap, sizeof(sr_packet)))) return rc;
-    if (!c->d_fill && hipMalloc(&c->d_fill, (2 * (size_t)c->ds.nds + 2) * sizeof(uint16_t)) != hipSuccess)
-        return -ENOMEM;
-    if (!c->d_mcounts && hipMalloc(&c->d_mcounts, 4 * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
-    const size_t nds = c->ds.nds;
-    if (hipMemcpyAsync(c->d_in, bytes, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return -EIO;
-    if (nds && hipMemcpyAsync(c->d_fill, fill, nds * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream) != hipSuccess)
-        return -EIO;
-    RouteParams p = c->ds.params();
-    DeviceState::add_batch(p, c->d_in, nbytes, c->d_out, cap, nullptr, c->d_count, c->d_probed);
-    if ((rc = launch_variant(c->ds, p, c->stream))) return rc;
-    if ((rc = sr_pack_packets(c, c->d_out, c->d_count, cap, c->d_fill, c->ds.dead ? c->d_probed : nullptr,
-                              c->d_sorted, c->d_packets, pcap, c->d_mcounts, c->d_fill + nds)))
-        return rc;
-    uint64_t cnt[3] = {0, 0, 0};
-    if (hipMemcpyAsync(cnt, c->d_mcounts, sizeof(cnt), hipMemcpyDeviceToHost, c->stream) != hipSuccess) return -EIO;
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return -EIO;
-    const size_t nr = (size_t)cnt[2], np = (size_t)cnt[0];
-    const size_t cr = nr < max_records ? nr : max_records, cp = np < max_packets ? np : max_packets;
-    if (cr && hipMemcpyAsync(sorted, c->d_sorted, cr * sizeof(sr_record), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
-        return -EIO;
-    if (cp && hipMemcpyAsync(packets, c->d_packets, cp * sizeof(sr_packet), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
-        return -EIO;
-    if (nds && hipMemcpyAsync(fill, c->d_fill + nds, nds * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
-        return -EIO;
-    if (probed_dead && nw) {
-        if (c->ds.dead) {
-            if (hipMemcpyAsync(probed_dead, c->d_probed, nw * sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream) !=
-                hipSuccess)
-                return -EIO;
-        } else {
-            memset(probed_dead, 0, nw * sizeof(uint64_t));
-        }
-    }
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return -EIO;
-    *n_records = nr;
-    *n_valid = (size_t)cnt[1];
-    *n_packets = np;
-    return (nr > max_records || np > max_packets) ? -ENOSPC : 0;
+    int rc = pack_submit(c, 2, bytes, nbytes, fill);
+    if (rc) return rc;
+    sr_pack_result r;
+    rc = pack_result(c, 2, &r);
+    if (rc && rc != -ENOSPC) return rc;
+    const size_t cr = r.n_records < max_records ? r.n_records : max_records;
+    const size_t cp = r.n_packets < max_packets ? r.n_packets : max_packets;
+    if (cr) memcpy(sorted, r.sorted, cr * sizeof(sr_record));
+    if (cp) memcpy(packets, r.packets, cp * sizeof(sr_packet));
+    if (c->ds.nds) memcpy(fill, r.fill, c->ds.nds * sizeof(uint16_t));
+    if (probed_dead && nw) memcpy(probed_dead, r.probed_dead, nw * sizeof(uint64_t));
+    *n_records = r.n_records;
+    *n_valid = r.n_valid;
+    *n_packets = r.n_packets;
+    return (rc || r.n_records > max_records || r.n_packets > max_packets) ? -ENOSPC : 0;
 }
 
 int sr_route_batch(sr_ctx *c, const uint8_t *bytes, size_t nbytes, sr_record *out, size_t max_records,

@@ -119,6 +119,52 @@ def test_route_pack_chained_batches(pkg, oracle):
             assert [len(pend_g.get(k, b"")) for k in range(n)] == list(map(int, fill_g))
 
 
+def test_route_pack_submit_double_buffered(pkg, oracle):
+    """sr_route_pack_submit / sr_route_pack_result on alternating slots, each result taken after the
+    next batch was submitted, the pending bytes chained on the device (fill None) except where the
+    host sets them: every batch equals the oracle's chain (records, descriptors, fills, probed dead)."""
+    n = 7
+    rng = np.random.default_rng(11)
+    fill_o = [0] * n
+    expect = []
+    with pkg.Router(n, 1 << 18) as r:
+        inflight = None
+        for b in range(14):
+            alive = (rng.random(n) > 0.3).astype(int).tolist()
+            s = pkg.gen_stream(int(rng.integers(1, 1 << 18)), [6, 64, 300, 1449], seed=300 + b, p_invalid=0.05)
+            host_fill = None
+            if b in (0, 6):   # the host sets the pending bytes (a flush timer, a ping) now and then
+                host_fill = rng.integers(0, 1451, n).tolist()
+                if inflight is not None:   # the chain must be drained before the host's fills apply
+                    got = r.route_pack_result(inflight[0])
+                    assert_pack_equal(got, inflight[1])
+                    inflight = None
+                fill_o = host_fill
+            r.set_alive(alive)
+            slot = b % 2
+            r.route_pack_submit(slot, s.data, host_fill)
+            recs, _, _ = oracle.route(s.data, n, alive)
+            probed = oracle.probed_dead(s.data, n, alive)
+            srt_o, pk_o, fo_o, nv_o = oracle.pack_packets(recs, n, fill_o, probed)
+            fill_o = list(map(int, fo_o))
+            if inflight is not None:
+                assert_pack_equal(r.route_pack_result(inflight[0]), inflight[1])
+            inflight = (slot, (srt_o, pk_o, fo_o, nv_o, probed))
+        assert_pack_equal(r.route_pack_result(inflight[0]), inflight[1])
+        with pytest.raises(pkg.SrError):   # a slot's result is taken once
+            r.route_pack_result(inflight[0])
+
+
+def assert_pack_equal(got, want):
+    srt, pk, fo, nv, pr = got
+    srt_o, pk_o, fo_o, nv_o, probed = want
+    assert pr.tolist() == probed.tolist()
+    assert nv == nv_o
+    assert np.array_equal(srt, srt_o), "sorted records differ"
+    assert np.array_equal(pk.view(np.uint8), pk_o.view(np.uint8)), "packet descriptors differ"
+    assert np.array_equal(fo, fo_o), "pending bytes after the batch differ"
+
+
 def test_pack_packets_device_many(pkg, oracle, torch_stream):
     """Several batches routed in one sr_route_device_many launch (with probed-dead bitmaps), then
     sr_pack_packets per batch on device buffers, the pending bytes chained on the device."""

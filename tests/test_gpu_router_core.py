@@ -2,7 +2,7 @@
 packing on the device) replays the scripted sessions the compiled reference ran
 (tests/golden/router_*.json): every packet each downstream received, every WARN line, the final
 pending buffers and counters must be identical, whether each datagram is its own batch or
-consecutive datagrams share one."""
+consecutive datagrams share one, synchronous or double-buffered."""
 from __future__ import annotations
 
 import importlib
@@ -14,7 +14,7 @@ from conftest import load_router_fixture, router_fixtures
 pytestmark = pytest.mark.gpu
 
 
-def _replay(pkg, f, group: int, in_place: bool):
+def _replay(pkg, f, group: int, mode: str):
     core_mod = importlib.import_module("statsd-router_amd.core")
     core = core_mod.Core(f["n"], f["ds_hosts"], f["ds_data_ports"], f["ping_prefix"], f["hostname"], f["data_port"],
                          max_batch_bytes=1 << 20)
@@ -23,7 +23,7 @@ def _replay(pkg, f, group: int, in_place: bool):
     def flush_batch():
         if pend:
             framed = pkg.frame_datagrams(pend)
-            (core.route_in_place if in_place else core.route)(framed)
+            {"copy": core.route, "in_place": core.route_in_place, "async": core.submit}[mode](framed)
             pend.clear()
 
     for e in f["events"]:
@@ -40,16 +40,20 @@ def _replay(pkg, f, group: int, in_place: bool):
         elif e[0] == "ping":
             core.ping()
     flush_batch()
+    core.drain()
     final = {s: core.state(s) for s in range(f["n"])}
     core.close()
     return core, final
 
 
-@pytest.mark.parametrize("group", [1, 7, 1000])
+@pytest.mark.parametrize("group,mode", [(1, "copy"), (7, "in_place"), (1000, "copy"), (1, "async"), (7, "async"),
+                                        (1000, "async")])
 @pytest.mark.parametrize("name", router_fixtures())
-def test_core_replays_reference_session(pkg, name, group):
+def test_core_replays_reference_session(pkg, name, group, mode):
+    """mode "async": double-buffered (sr_core_submit / sr_core_drain), every batch completing while
+    the next one is on the GPU, pending bytes chained on the device."""
     f = load_router_fixture(name)
-    core, final = _replay(pkg, f, group, in_place=group == 7)
+    core, final = _replay(pkg, f, group, mode)
     assert core.logs == f["logs"]
     assert {k: v for k, v in core.packets.items() if v} == f["packets"]
     assert final == f["final"]

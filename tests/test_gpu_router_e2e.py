@@ -139,3 +139,44 @@ def test_router_matches_reference_executable(tmp_path):
     ref, w2 = run_router(REFERENCE, dg, 3, str(tmp_path))
     assert ours == ref
     assert w1 == w2
+
+
+def test_timers_run_while_the_socket_never_drains(tmp_path):
+    """Two blasters saturate the data port for 3 s: the read event hands back to the loop after a few
+    batches (sr_router_main.c), so the ping timer (0.3 s) still fires and its self-metrics reach the
+    downstream among the data packets, as the reference's one-datagram reads let its timers run."""
+    blast = os.path.join(REPO, "tools", "loopback", "sr_blast")
+    base = free_ports(6)
+    data_port, ctl, sink_base = base, base + 1, base + 2
+    dump = os.path.join(str(tmp_path), "dump-saturated.bin")
+    sink = subprocess.Popen([SINK, str(sink_base), "1", "12", "1.5", dump], stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE)
+    assert sink.stderr.readline().strip() == b"ready"
+    r = Router(OURS, config_text(data_port, ctl, [(sink_base, sink_base + 1)], log_level=1, flush=1.0, health=0.2,
+                                 ping=0.3, prefix=PREFIX), str(tmp_path))
+    try:
+        assert r.wait_for(lambda lv, m: m == b"ds_health_read_cb downstream 0 is up", 20), r.raw[-20:]
+        time.sleep(0.5)
+        bl = [subprocess.Popen([blast, str(data_port), "3", "0", "1400", str(40 + k)], stdout=subprocess.PIPE)
+              for k in range(2)]
+        for b in bl:
+            b.communicate(timeout=60)
+        sink.communicate(timeout=60)
+    finally:
+        r.stop()
+        if sink.poll() is None:
+            sink.kill()
+    with open(dump, "rb") as f:
+        blob = f.read()
+    seq, i = [], 0   # per datagram: (data lines, healthy_downstreams gauge lines)
+    while i < len(blob):
+        l = int.from_bytes(blob[i + 2:i + 4], "little")
+        lines = blob[i + 4:i + 4 + l].split(b"\n")[:-1]
+        i += 4 + l
+        seq.append((sum(not x.startswith(PREFIX.encode()) for x in lines),
+                    sum(x.startswith(PREFIX.encode()) and b"healthy_downstreams" in x for x in lines)))
+    data_idx = [k for k, (d, _) in enumerate(seq) if d]
+    assert len(data_idx) > 1000, "the blast never reached the downstream"
+    first, last = data_idx[0], data_idx[-1]
+    during = sum(g for d, g in seq[first:last + 1])
+    assert during >= 4, f"only {during} ping gauges among {last - first + 1} datagrams of a 3 s blast (ping 0.3 s)"

@@ -14,6 +14,8 @@ import pytest
 from router_proc import OURS, REFERENCE, HealthServer, Router, config_text, control, free_ports
 
 BOTH = [OURS] + ([REFERENCE] if os.path.exists(REFERENCE) else [])
+# on a CPU box our data threads cannot open a GPU context: keep the main thread's services running
+NO_GPU = {"SR_REQUIRE_GPU": "0"}
 
 
 def _msgs(r):
@@ -55,7 +57,7 @@ BAD = {
 def test_bad_config_same_as_reference(tmp_path, name):
     out = {}
     for exe in (OURS, REFERENCE):
-        r = Router(exe, BAD[name], str(tmp_path))
+        r = Router(exe, BAD[name], str(tmp_path), env=NO_GPU)
         rc = r.wait_exit(10)
         out[exe] = (rc, _msgs(r))
     assert out[OURS] == out[REFERENCE]
@@ -63,7 +65,7 @@ def test_bad_config_same_as_reference(tmp_path, name):
 
 
 def test_bad_config_messages(tmp_path):
-    r = Router(OURS, BAD["empty_line"], str(tmp_path))
+    r = Router(OURS, BAD["empty_line"], str(tmp_path), env=NO_GPU)
     assert r.wait_exit(10) == 1
     assert ("ERROR", b'process_config_line: bad line in config ""') in r.lines
     assert ("ERROR", b"init_config: failed to load config file") in r.lines
@@ -74,7 +76,7 @@ def test_bad_config_messages(tmp_path):
 def test_control_port_health_replies(tmp_path, exe):
     """test/020: health -> "health: up"; "health down" sets a sticky reply; unknown -> nothing."""
     base = free_ports(4)
-    r = Router(exe, config_text(base, base + 1, [(base + 2, base + 3)], log_level=3), str(tmp_path))
+    r = Router(exe, config_text(base, base + 1, [(base + 2, base + 3)], log_level=3), str(tmp_path), env=NO_GPU)
     try:
         time.sleep(0.3)
         assert control(base + 1, b"health\n") == b"health: up\n"
@@ -95,7 +97,7 @@ def test_downstream_health_toggles(tmp_path, exe):
     base = free_ports(8)
     ds = [(base + 2 + 2 * i, base + 3 + 2 * i) for i in range(3)]
     hs = [HealthServer(h) for _, h in ds]
-    r = Router(exe, config_text(base, base + 1, ds, log_level=1, health=0.1), str(tmp_path))
+    r = Router(exe, config_text(base, base + 1, ds, log_level=1, health=0.1), str(tmp_path), env=NO_GPU)
     try:
         for i in (0, 2):
             hs[i].start()
@@ -110,3 +112,40 @@ def test_downstream_health_toggles(tmp_path, exe):
         r.stop()
         for h in hs:
             h.stop()
+
+
+@pytest.mark.parametrize("exe", BOTH)
+def test_sighup_sigint(tmp_path, exe):
+    """sr-init.c:177-185,290-297: SIGHUP is logged at INFO and the router keeps serving; SIGINT is logged
+    and the process exits with status 0. Same lines from both executables."""
+    import signal
+
+    base = free_ports(4)
+    r = Router(exe, config_text(base, base + 1, [(base + 2, base + 3)], log_level=2), str(tmp_path), env=NO_GPU)
+    try:
+        time.sleep(0.3)
+        r.p.send_signal(signal.SIGHUP)
+        assert r.wait_for(lambda lv, m: (lv, m) == ("INFO", b"on_sighup: sighup received"), 5)
+        assert r.p.poll() is None
+        assert control(base + 1, b"health\n") == b"health: up\n"
+        r.p.send_signal(signal.SIGHUP)
+        time.sleep(0.2)
+        assert sum(m == b"on_sighup: sighup received" for _, m in r.lines) == 2
+        r.p.send_signal(signal.SIGINT)
+        assert r.wait_exit(10) == 0
+        assert ("INFO", b"on_sigint: sigint received") in r.lines
+    finally:
+        r.stop()
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="needs a box without a GPU")
+def test_data_thread_without_gpu_ends_the_process(tmp_path):
+    """A data thread that cannot open its GPU context must not leave its SO_REUSEPORT share of the
+    data port unread while the control port answers "health: up": the process exits with status 1."""
+    base = free_ports(4)
+    r = Router(OURS, config_text(base, base + 1, [(base + 2, base + 3)], log_level=3), str(tmp_path))
+    try:
+        assert r.wait_exit(30) == 1
+        assert any(lv == "ERROR" and m.startswith(b"data_pipe_thread: sr_core_open() failed") for lv, m in r.lines)
+    finally:
+        r.stop()

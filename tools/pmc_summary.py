@@ -47,10 +47,16 @@ def main():
         res["hbm_bytes_per_launch"] = rd + wr
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
+    # the build the counters were taken on (bench.py reports them only for the same library)
+    import hashlib
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "statsd-router_amd", "lib",
+                       "libsr_route.so")
+    if os.path.exists(lib):
+        res["lib_sha256"] = hashlib.sha256(open(lib, "rb").read()).hexdigest()
     if traffic_out and "hbm_bytes_per_launch" in res:
         with open(traffic_out, "w") as fh:
-            json.dump({k: res[k] for k in ("config", "kernel", "hbm_bytes_per_launch", "hbm_read_bytes_per_launch",
-                                           "hbm_write_bytes_per_launch", "dispatches")}, fh, indent=1)
+            json.dump({k: res.get(k) for k in ("config", "kernel", "hbm_bytes_per_launch", "hbm_read_bytes_per_launch",
+                                               "hbm_write_bytes_per_launch", "dispatches", "lib_sha256")}, fh, indent=1)
     print(json.dumps(res))
 
 
