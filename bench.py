@@ -329,7 +329,8 @@ def main(argv=None):
         if not args.no_e2e:
             result["e2e"] = e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M)
         if not args.no_pack:
-            result["route_pack"] = pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev)
+            result["route_pack"] = pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev,
+                                            dead=sum(alive) < shards)
     router.close()
     del d_in, d_out
     torch.cuda.empty_cache()
@@ -593,7 +594,7 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8, exchange="
                      f"trip per step for the split sizes")}
 
 
-def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev, reps=20):
+def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev, dead=False, reps=20):
     """The router's device data path: one route launch over M batches (the
     batches of M data threads), then the per-downstream MTU packing of all of them in one
     sr_pack_packets_many (sorted records + packet descriptors, each batch from its own pending
@@ -613,11 +614,14 @@ def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, de
     # the probed-dead bitmap of every batch, as the router asks for it (sr-main.c:106; with every shard
     # alive the route launch skips it)
     d_pd = torch.zeros((M, max((shards + 63) // 64, 1)), dtype=torch.int64, device=dev)
+    # with dead shards the router has the route kernel write the hashes (the replay reads them)
+    d_h = torch.empty((M, max_lines), dtype=torch.int64, device=dev) if dead else None
     base = d_in.data_ptr()
 
     def route():
-        router.route_device_many([(base + b * batch_bytes, sizes[b], d_rec[b].data_ptr(), max_lines, None,
-                                   d_cnt[b].data_ptr(), d_pd[b].data_ptr()) for b in range(M)])
+        router.route_device_many([(base + b * batch_bytes, sizes[b], d_rec[b].data_ptr(), max_lines,
+                                   d_h[b].data_ptr() if dead else None, d_cnt[b].data_ptr(), d_pd[b].data_ptr())
+                                  for b in range(M)])
 
     def pack():   # the batches of M data threads: independent pending bytes, one set of launches
         router.pack_packets_many([(d_rec[b].data_ptr(), d_cnt[b].data_ptr(), max_lines, d_fill[b].data_ptr(),

@@ -178,6 +178,14 @@ int sr_core_open(sr_core **out, const sr_core_config *cfg, sr_core_emit_fn emit,
         sr_core_close(c);
         return rc;
     }
+    /* both slots' buffers allocated now (an empty batch each), not while the socket fills */
+    for (int k = 0; k < 2; k++) {
+        sr_pack_result r;
+        if ((rc = sr_route_pack_submit(c->ctx, k, NULL, 0, c->fill16)) || (rc = sr_route_pack_result(c->ctx, k, &r))) {
+            sr_core_close(c);
+            return rc;
+        }
+    }
     build_names(c, cfg);
     *out = c;
     return 0;

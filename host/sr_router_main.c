@@ -35,6 +35,7 @@ typedef struct data_thread {
     sr_config *c;
     struct ev_loop *loop;
     ev_io io;
+    ev_idle idle;            /* completes the batch in flight once the loop has nothing else to do */
     ev_periodic flush_timer, ping_timer;
     sr_core *core;
     int sock_in;
@@ -113,9 +114,10 @@ static void refresh_alive(data_thread *d) {
     if (rc) sr_log(SR_ERROR, "%s: sr_core_set_alive() failed %s", "data_pipe_thread", strerror(-rc));
 }
 
-/* A read event's batches go to the GPU while the next ones are received (sr_core_submit: slot k routes
- * while slot k^1 fills and the batch before it is walked and sent); the event ends with the last batch
- * drained, so a lone datagram still costs one GPU round trip. */
+/* A read event's batch goes to the GPU while the next one is received (sr_core_submit: slot k routes
+ * while slot k^1 fills; the batch before it is walked and sent when k is submitted). A read event
+ * ends with its batch in flight: the next read event completes it, or, when the loop finds nothing
+ * else to do, the idle watcher does, so a lone datagram still costs about one GPU round trip. */
 static void submit_batch(data_thread *d) {
     if (!d->len) return;
     refresh_alive(d);
@@ -127,8 +129,14 @@ static void submit_batch(data_thread *d) {
 }
 
 static void drain(data_thread *d) {
+    ev_idle_stop(d->loop, &d->idle);
     int rc = sr_core_drain(d->core);
     if (rc) sr_log(SR_ERROR, "%s: sr_core_drain() failed %s", "udp_read_cb", strerror(-rc));
+}
+
+static void idle_cb(struct ev_loop *loop, ev_idle *w, int revents) {
+    (void)loop, (void)revents;
+    drain((data_thread *)((char *)w - offsetof(data_thread, idle)));
 }
 
 static void route_batch(data_thread *d) {
@@ -178,7 +186,8 @@ static void udp_read_cb(struct ev_loop *loop, ev_io *w, int revents) {
         }
         if (k < RECV_VLEN) break;   /* drained */
     }
-    route_batch(d);
+    submit_batch(d);
+    ev_idle_start(d->loop, &d->idle);
 }
 
 static void flush_timer_cb(struct ev_loop *loop, ev_periodic *p, int revents) {
@@ -278,6 +287,7 @@ void *sr_data_thread(void *arg) {
     refresh_alive(d);
     ev_io_init(&d->io, udp_read_cb, d->sock_in, EV_READ);
     ev_io_start(d->loop, &d->io);
+    ev_idle_init(&d->idle, idle_cb);
     ev_periodic_init(&d->flush_timer, flush_timer_cb, 0.0, c->downstream_flush_interval, 0);
     ev_periodic_start(d->loop, &d->flush_timer);
     ev_periodic_init(&d->ping_timer, ping_timer_cb, 0.0, c->downstream_ping_interval, 0);

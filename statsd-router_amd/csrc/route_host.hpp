@@ -273,22 +273,19 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
     RouteParams p = in;
     p.nb = 0;
     bool replay = false;   // some batch asked for the probed-dead bitmap (probed_dead_kernel)
+    p.nwords = ds.nwords;
     for (uint32_t i = 0; i < in.nb; ++i) {
-        // the probed-dead bitmap starts empty; with every shard alive nothing can set it
-        if (in.b[i].probed_dead) {
-            if (hipMemsetAsync(in.b[i].probed_dead, 0, (size_t)(ds.nwords ? ds.nwords : 1) * sizeof(uint64_t),
+        if (in.b[i].nbytes == 0) {   // no tile, no scanner: its count and bitmap are set here
+            if (hipMemsetAsync(in.b[i].n_out, 0, sizeof(uint64_t), stream) != hipSuccess) return -EIO;
+            if (in.b[i].probed_dead &&
+                hipMemsetAsync(in.b[i].probed_dead, 0, (size_t)(ds.nwords ? ds.nwords : 1) * sizeof(uint64_t),
                                stream) != hipSuccess)
                 return -EIO;
-        }
-    }
-    for (uint32_t i = 0; i < in.nb; ++i) {
-        if (in.b[i].nbytes == 0) {
-            if (hipMemsetAsync(in.b[i].n_out, 0, sizeof(uint64_t), stream) != hipSuccess) return -EIO;
             continue;
         }
+        // the batch's scanner zeroes its bitmap; with every shard alive nothing sets it afterwards
         p.b[p.nb++] = in.b[i];
-        if (ds.dead == 0) p.b[p.nb - 1].probed_dead = nullptr;
-        if (p.b[p.nb - 1].probed_dead) replay = true;
+        if (ds.dead && p.b[p.nb - 1].probed_dead) replay = true;
     }
     if (p.nb == 0) return 0;
     // 8+ batches: each batch's tiles on one XCD class; its scanner (block j) shares that class

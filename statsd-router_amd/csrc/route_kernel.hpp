@@ -168,7 +168,7 @@ struct RouteParams {
     uint32_t dead;           // dead downstreams in the alive snapshot
     uint32_t pending_cap;
     uint32_t nwords_check;   // probed_dead_kernel: bitmap words checked for completion (0: never)
-    uint32_t pad_nw;
+    uint32_t nwords;         // alive / probed-dead bitmap words
     Magic magic_n;           // for h % nds (fast path)
     const uint64_t *alive;   // bitmap
     const Magic *magic;      // [0..nds], index i -> divisor i
@@ -552,9 +552,32 @@ __device__ __forceinline__ Magic magic_from_pad(const uint32_t *img, uint32_t e)
     return mg;
 }
 
+// The alive bitmap's first kAliveLds words sit in the pad dwords of image rows kAliveRow0 ..
+// (word w: rows kAliveRow0 + 2w, + 1 for its high half), so that the probe's alive tests read LDS:
+// a global load inside the line loop would also wait for every record store issued before it.
+constexpr uint32_t kAliveRow0 = 4 * kMagicLds;
+constexpr uint32_t kAliveLds = 16;   // words: up to 1024 downstreams
+__device__ __forceinline__ uint32_t alive_pad_dword(const uint32_t *img, uint32_t k) {
+    return img[(kAliveRow0 + (k >> 5)) * 17 + 16];
+}
+
+// note_dead with a workgroup's LDS copy of the bitmap in front (shards below 64 * kReplayCheckWords):
+// only the first lane of the workgroup to probe a dead shard touches the global word. The global
+// words are the hot addresses of a replay; same-address agent-scope traffic from every wave would
+// serialise at the memory side.
+constexpr uint32_t kReplayCheckWords = 16;   // workgroup-local bitmap words (up to 1024 shards)
+__device__ __forceinline__ void note_dead_wg(uint64_t *pd, unsigned long long *wg, uint32_t k) {
+    if (wg && k < 64 * kReplayCheckWords) {
+        const unsigned long long bit = 1ull << (k & 63);
+        if (wg[k >> 6] & bit) return;
+        if (atomicOr(&wg[k >> 6], bit) & bit) return;
+    }
+    note_dead(pd, k);
+}
+
 template <bool MARK = false>
 __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark = nullptr,
-                                const uint32_t *pad_img = nullptr) {
+                                const uint32_t *pad_img = nullptr, unsigned long long *mark_wg = nullptr) {
     const uint32_t n = p.nds;
     if (p.dead >= n) {                                    // includes N == 0
         if (MARK && n) note_all_dead(mark, n);
@@ -562,8 +585,15 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark
     }
     if (p.dead == 0) return mod_magic(h, p.magic_n, n);   // every shard alive: j = h % N
     // up to 64 shards the alive bitmap is one word, read once per probe
-    const uint64_t alive0 = n <= 64 ? p.alive[0] : 0ull;
-    auto alive_k = [&](uint32_t k) { return n <= 64 ? ((alive0 >> k) & 1ull) != 0 : alive_bit(p.alive, k); };
+    const bool lds_alive = pad_img && n <= 64 * kAliveLds;
+    const uint64_t alive0 = n > 64 ? 0ull
+                            : lds_alive ? ((uint64_t)alive_pad_dword(pad_img, 32) << 32) | alive_pad_dword(pad_img, 0)
+                                        : p.alive[0];
+    auto alive_k = [&](uint32_t k) {
+        if (n <= 64) return ((alive0 >> k) & 1ull) != 0;
+        if (lds_alive) return ((alive_pad_dword(pad_img, k) >> (k & 31)) & 1u) != 0;
+        return alive_bit(p.alive, k);
+    };
     auto magic_i = [&](uint32_t i) {
         return (pad_img && n - i < kMagicLds) ? magic_from_pad(pad_img, n - i) : p.magic[i];
     };
@@ -576,7 +606,7 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark
         const uint32_t j = mod_magic(h, magic_i(i), i);                                  // :98
         const uint32_t k = (o0 >> 16) == j ? (o0 & 0xFFFFu) : j;                         // :99
         if (alive_k(k)) return k;                                                         // :101-104
-        if (MARK) note_dead(mark, k);                                                     // :106
+        if (MARK) note_dead_wg(mark, mark_wg, k);                                         // :106
         if (j != i - 1) {                                                                 // :108-111
             const uint32_t v = (o0 >> 16) == i - 1 ? (o0 & 0xFFFFu) : i - 1;
             if (o0 == 0xFFFFFFFFu) o0 = (j << 16) | v;
@@ -595,7 +625,7 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark
         for (int e = 0; e < kOverlay; ++e)
             if ((ov[e] >> 16) == j) k = ov[e] & 0xFFFFu;
         if (alive_k(k)) return k;                                    // :101-104
-        if (MARK) note_dead(mark, k);                                // :106
+        if (MARK) note_dead_wg(mark, mark_wg, k);                    // :106
         if (j != i - 1) {                                            // :108-111
             uint32_t v = i - 1;
 #pragma unroll
@@ -1656,6 +1686,10 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
         // the scanner is the latency-critical link of every tile's record base: its few
         // instructions go ahead of the co-resident tiles' VALU work
         __builtin_amdgcn_s_setprio(3);
+        // the batch's probed-dead bitmap starts empty (set after this launch by probe_wide_kernel and
+        // probed_dead_kernel, sr-main.c:106; with every shard alive it stays empty)
+        if (uint64_t *pd = p.b[blockIdx.x].probed_dead)
+            for (uint32_t w = tid; w < p.nwords; w += BLOCK) pd[w] = 0ull;
         const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (ABL & ABL_OLD_SCANNER) {
             if (wave == 0) scan_batch<BLOCK>(p, p.b[blockIdx.x], ep0, lane);
@@ -1704,6 +1738,9 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
         const uint32_t e = (uint32_t)tid >> 2;   // divisor nds - e >= 1: entries e < nds only
         if (e < p.nds) sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)&p.magic[p.nds - e])[tid & 3];
     }
+    if (p.dead && p.dead < p.nds && p.nds <= 64 * kAliveLds && tid >= (int)kAliveRow0 &&
+        (uint32_t)tid < kAliveRow0 + 2 * ((p.nds + 63) / 64))   // the alive words (probe_shard)
+        sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)p.alive)[tid - kAliveRow0];
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
     uint64_t nlm, clm;
     uint32_t c_in;
@@ -1759,45 +1796,62 @@ __global__ __launch_bounds__(64) void probe_wide_kernel(RouteParams p) {
 // resolved by probe_wide_kernel, which sets their bits itself.
 // The bitmap can only ever hold the snapshot's dead shards, and in a large batch every one of them is
 // some line's first pick within the first few thousand lines: kReplayBlocks workgroups per batch
-// (grid y = batch) stride over its records and stop as soon as the bitmap holds every dead shard
-// (checked per stride, a few L2 reads), so the replay re-hashes a few thousand lines, not the batch.
+// (grid y = batch) stride over its records and stop as soon as the bitmap holds every dead shard.
+// Each workgroup keeps its own copy of the bitmap in LDS: a lane notes a dead shard in the global
+// word only when it is new to the workgroup, and one lane per stride reads the global words for the
+// completion test (N <= 1024; beyond that the replay runs over every record).
 constexpr uint32_t kReplayBlocks = 32;
-constexpr uint32_t kReplayCheckWords = 16;   // bitmaps up to 1024 shards are checked for completion
-
-__device__ __forceinline__ bool all_dead_noted(const RouteParams &p, const uint64_t *pd) {
-    if (p.nwords_check == 0) return false;
-    for (uint32_t w = 0; w < p.nwords_check; ++w) {
-        const uint32_t hi = p.nds - 64 * w;
-        const uint64_t full = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
-        const uint64_t seen = __hip_atomic_load(pd + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | p.alive[w];
-        if ((seen & full) != full) return false;
-    }
-    return true;
-}
 
 __global__ __launch_bounds__(256) void probed_dead_kernel(RouteParams p) {
+    __shared__ unsigned long long wg[kReplayCheckWords];
+    __shared__ uint32_t complete;
     const uint32_t bi = blockIdx.y;
     if (bi >= p.nb) return;
     const BatchDesc &bd = p.b[bi];
     if (!bd.probed_dead) return;
+    const uint32_t nw = p.nwords_check;   // 0: no workgroup copy, no completion test
+    if (threadIdx.x < kReplayCheckWords) wg[threadIdx.x] = 0ull;
     const uint32_t n = (uint32_t)min(*bd.n_out, (uint64_t)bd.max_records);
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
     for (uint32_t i0 = blockIdx.x * 256u; i0 < n; i0 += gridDim.x * 256u) {
-        if (all_dead_noted(p, bd.probed_dead)) return;   // the same answer for every lane
+        __syncthreads();
+        if (threadIdx.x == 0) {   // every dead shard already noted (by any workgroup): nothing left to add
+            bool all = nw != 0;
+            for (uint32_t w = 0; w < nw && all; ++w) {
+                const uint32_t hi = p.nds - 64 * w;
+                const uint64_t full = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+                uint64_t seen = wg[w] | p.alive[w];
+                if ((seen & full) != full)
+                    seen |= __hip_atomic_load(bd.probed_dead + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                all = (seen & full) == full;
+            }
+            complete = all ? 1u : 0u;
+        }
+        __syncthreads();
+        if (complete) return;
         const uint32_t i = i0 + threadIdx.x;
         if (i >= n) continue;
         const sr_record r = bd.recs[i];
         if (r.route == SR_ROUTE_INVALID_LENGTH || r.route == SR_ROUTE_INVALID_FORMAT) continue;
         if (r.route == SR_ROUTE_ALL_DEAD) {   // every shard dead: the probe visited all of them
-            if (p.dead >= p.nds && p.nds) note_all_dead(bd.probed_dead, p.nds);
+            if (p.dead >= p.nds && p.nds) {
+                if (nw) {
+                    for (uint32_t w = 0; w < nw; ++w) {
+                        const uint32_t hi = p.nds - 64 * w;
+                        wg[w] = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+                    }
+                }
+                note_all_dead(bd.probed_dead, p.nds);
+            }
             continue;
         }
-        // sdbm over the bytes before the first ':' (sr-main.c:120-134); the record is valid, so a
-        // ':' lies within the line
+        // sdbm over the bytes before the first ':' (sr-main.c:120-134): the route kernel's own when it
+        // wrote them, else recomputed (the record is valid, so a ':' lies within the line)
         uint64_t h = 0;
         const uint32_t a0 = r.offset & ~3u, end = r.offset + r.length;
-        bool done = false;
+        bool done = bd.hashes != nullptr;
+        if (done) h = bd.hashes[i];
         for (uint32_t a = a0; a < end && !done; a += 4) {
             const uint32_t x = __builtin_amdgcn_raw_buffer_load_b32(rsrc, a, 0, 0);
 #pragma unroll
@@ -1810,7 +1864,7 @@ __global__ __launch_bounds__(256) void probed_dead_kernel(RouteParams p) {
                 }
             }
         }
-        (void)probe_shard<true>(h, p, bd.probed_dead);
+        (void)probe_shard<true>(h, p, bd.probed_dead, nullptr, nw ? wg : nullptr);
     }
 }
 

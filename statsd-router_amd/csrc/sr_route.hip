@@ -528,12 +528,16 @@ static int pack_submit(sr_ctx *c, int k, const uint8_t *bytes, size_t nbytes, co
     (void)hipSetDevice(c->device);
     const size_t nds = c->ds.nds, nw = c->ds.nwords;
     int rc;
-    if ((rc = slot_reserve(c, k, nbytes ? nbytes : 1))) return rc;
+    // every buffer is sized for the context's largest batch at the first submission (an empty one
+    // pre-allocates): growing page-locked memory or freeing device memory mid-stream would stall the
+    // data thread while its socket fills
+    const size_t full = c->ds.max_batch, fullp = (size_t)SR_MAX_PACKETS(full, nds);
+    if ((rc = slot_reserve(c, k, full))) return rc;
     const size_t cap = nbytes ? nbytes : 1;   // never more lines than bytes
     const size_t pcap = (size_t)SR_MAX_PACKETS(cap, nds);
-    if ((rc = grow((void **)&c->d_out, &c->d_out_cap, cap, sizeof(sr_record)))) return rc;
-    if ((rc = grow((void **)&c->d_sorted, &c->d_sorted_cap, cap, sizeof(sr_record)))) return rc;
-    if ((rc = grow((void **)&c->d_packets, &c->d_packets_cap, pcap, sizeof(sr_packet)))) return rc;
+    if ((rc = grow((void **)&c->d_out, &c->d_out_cap, full, sizeof(sr_record)))) return rc;
+    if ((rc = grow((void **)&c->d_sorted, &c->d_sorted_cap, full, sizeof(sr_record)))) return rc;
+    if ((rc = grow((void **)&c->d_packets, &c->d_packets_cap, fullp, sizeof(sr_packet)))) return rc;
     if (!c->d_fill) {
         if (hipMalloc(&c->d_fill, (3 * nds + 2) * sizeof(uint16_t)) != hipSuccess) {
             c->d_fill = nullptr;
@@ -556,8 +560,15 @@ static int pack_submit(sr_ctx *c, int k, const uint8_t *bytes, size_t nbytes, co
         if (hipMemsetAsync(c->d_mcounts, 0, 4 * sizeof(uint64_t), c->stream) != hipSuccess) return -EIO;
     } else {
         if (hipMemcpyAsync(c->d_in, bytes, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return -EIO;
+        // with dead shards the route kernel also writes the hashes: the probed-dead replay then
+        // reads 8 bytes per line instead of re-hashing the names (probed_dead_kernel)
+        uint64_t *hashes = nullptr;
+        if (c->ds.dead) {
+            if ((rc = grow((void **)&c->d_hash, &c->d_hash_cap, full, sizeof(uint64_t)))) return rc;
+            hashes = c->d_hash;
+        }
         RouteParams p = c->ds.params();
-        DeviceState::add_batch(p, c->d_in, nbytes, c->d_out, cap, nullptr, c->d_count, c->d_probed);
+        DeviceState::add_batch(p, c->d_in, nbytes, c->d_out, cap, hashes, c->d_count, c->d_probed);
         if ((rc = launch_variant(c->ds, p, c->stream))) return rc;
         if ((rc = sr_pack_packets(c, c->d_out, c->d_count, cap, f_in, c->ds.dead ? c->d_probed : nullptr,
                                   c->d_sorted, c->d_packets, pcap, c->d_mcounts, f_out)))
@@ -667,7 +678,9 @@ int sr_route_batch(sr_ctx *c, const uint8_t *bytes, size_t nbytes, sr_record *ou
         if (hipMalloc(&c->d_out, cap * sizeof(sr_record)) != hipSuccess) return -ENOMEM;
         c->d_out_cap = cap;
     }
-    if (hashes && cap > c->d_hash_cap) {
+    // hashes: asked for, or (dead shards) for the probed-dead replay (probed_dead_kernel)
+    const bool want_hash = hashes || c->ds.dead;
+    if (want_hash && cap > c->d_hash_cap) {
         (void)hipFree(c->d_hash);
         c->d_hash = nullptr;
         c->d_hash_cap = 0;
@@ -676,7 +689,7 @@ int sr_route_batch(sr_ctx *c, const uint8_t *bytes, size_t nbytes, sr_record *ou
     }
     if (hipMemcpyAsync(c->d_in, bytes, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return -EIO;
     RouteParams p = c->ds.params();
-    DeviceState::add_batch(p, c->d_in, nbytes, c->d_out, cap, hashes ? c->d_hash : nullptr, c->d_count, c->d_probed);
+    DeviceState::add_batch(p, c->d_in, nbytes, c->d_out, cap, want_hash ? c->d_hash : nullptr, c->d_count, c->d_probed);
     int rc = launch_variant(c->ds, p, c->stream);
     if (rc) return rc;
     if (c->ds.dead && c->ds.nwords &&

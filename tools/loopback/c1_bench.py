@@ -68,13 +68,16 @@ def main():
     ap.add_argument("--dgram", type=int, default=1400)
     ap.add_argument("--only", choices=["ours", "reference"], default=None)
     ap.add_argument("--blasters", type=int, default=1, help="sender processes")
+    ap.add_argument("--exe", action="append", default=[],
+                    help="tag=path of another router executable to run the same way (A/B of builds)")
     a = ap.parse_args()
     import tempfile
 
     with tempfile.TemporaryDirectory() as tmp:
         exes = [("ours", OURS)] + ([("reference", REFERENCE)] if os.path.exists(REFERENCE) else [])
+        exes += [tuple(e.split("=", 1)) for e in a.exe]
         for tag, exe in exes:
-            if a.only and tag != a.only:
+            if a.only and tag != a.only and tag not in {e.split("=", 1)[0] for e in a.exe}:
                 continue
             print(json.dumps(dict(run(exe, a.seconds, a.threads, a.rate, a.dgram, tmp, nblast=a.blasters), kind=tag)), flush=True)
 
