@@ -225,25 +225,6 @@ void *sr_data_thread(void *arg) {
     d->t = t;
     d->c = c;
     d->sock_in = -1;
-    /* the GPU context first: no socket takes a share of the data port before this thread can route */
-    sr_core_config cc;
-    memset(&cc, 0, sizeof(cc));
-    cc.device = c->n_devices > 0 ? t->index % c->n_devices : 0;
-    cc.max_batch_bytes = c->batch_bytes;
-    cc.n_downstreams = (uint32_t)c->downstream_num;
-    cc.ds_hosts = (const char *const *)c->ds_hosts;
-    cc.ds_data_ports = (const char *const *)c->ds_data_ports;
-    cc.ping_prefix = c->ping_prefix;
-    cc.hostname = c->hostname;
-    cc.data_port = c->data_port + t->index;   /* sr-init.c:57,113 */
-    cc.log_level = sr_log_level;
-    int rc = sr_core_open(&d->core, &cc, on_emit, on_log, on_flush, d);
-    if (rc) {
-        sr_log(SR_ERROR, "%s: sr_core_open() failed %s", fn, strerror(-rc));
-        return thread_fail(d, 1);
-    }
-    d->slot = 0;
-    d->batch = sr_core_slot_buffer(d->core, 0, &d->cap);
     d->loop = ev_loop_new(0);
     d->sock_in = socket(PF_INET, SOCK_DGRAM, 0);
     if (d->sock_in < 0) {
@@ -266,6 +247,27 @@ void *sr_data_thread(void *arg) {
         sr_log(SR_ERROR, "%s: bind() failed %s", fn, strerror(errno));
         return thread_fail(d, 0);
     }
+    /* bound first (datagrams queue while the GPU context opens, as they do while the reference's
+     * thread starts); a thread whose GPU context cannot be opened closes its socket and ends the
+     * process, so no share of the port is left unread */
+    sr_core_config cc;
+    memset(&cc, 0, sizeof(cc));
+    cc.device = c->n_devices > 0 ? t->index % c->n_devices : 0;
+    cc.max_batch_bytes = c->batch_bytes;
+    cc.n_downstreams = (uint32_t)c->downstream_num;
+    cc.ds_hosts = (const char *const *)c->ds_hosts;
+    cc.ds_data_ports = (const char *const *)c->ds_data_ports;
+    cc.ping_prefix = c->ping_prefix;
+    cc.hostname = c->hostname;
+    cc.data_port = c->data_port + t->index;   /* sr-init.c:57,113 */
+    cc.log_level = sr_log_level;
+    int rc = sr_core_open(&d->core, &cc, on_emit, on_log, on_flush, d);
+    if (rc) {
+        sr_log(SR_ERROR, "%s: sr_core_open() failed %s", fn, strerror(-rc));
+        return thread_fail(d, 1);
+    }
+    d->slot = 0;
+    d->batch = sr_core_slot_buffer(d->core, 0, &d->cap);
     d->nout = c->socket_out_num;
     d->sock_out = calloc((size_t)d->nout, sizeof(int));
     d->smsg = calloc((size_t)d->nout * SEND_VLEN, sizeof(struct mmsghdr));

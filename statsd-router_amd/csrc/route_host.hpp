@@ -74,6 +74,8 @@ struct DeviceState {
     uint64_t *d_status = nullptr;
     uint64_t *d_bases = nullptr;
     PendingLine *d_pending = nullptr;
+    uint64_t *d_defer = nullptr;         // hashes of deferred probes by record index, for batches
+    size_t defer_cap = 0;                // routed without a hash array (two or more dead shards)
     // lane layout of the route kernel (SR_LAYOUT_*): AUTO follows the segment statistics that
     // KV_SEGMENTS launches publish into host-mapped memory (layout_out), probing now and then
     int layout_mode = 0;
@@ -142,6 +144,9 @@ struct DeviceState {
         (void)hipFree(d_status);
         (void)hipFree(d_bases);
         (void)hipFree(d_pending);
+        (void)hipFree(d_defer);
+        d_defer = nullptr;
+        defer_cap = 0;
         if (h_layout) (void)hipHostFree(h_layout);
         h_layout = nullptr;
         d_layout = nullptr;
@@ -178,6 +183,16 @@ struct DeviceState {
         }
         // the copy reads h_alive: complete it before the snapshot can change again
         return hipStreamSynchronize(stream) == hipSuccess ? 0 : -EIO;
+    }
+
+    int reserve_defer(size_t entries) {
+        if (entries <= defer_cap) return 0;
+        (void)hipFree(d_defer);
+        d_defer = nullptr;
+        defer_cap = 0;
+        if (hipMalloc(&d_defer, entries * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+        defer_cap = entries;
+        return 0;
     }
 
     // launch parameters without batches (add them with add_batch)
@@ -248,6 +263,7 @@ struct DeviceState {
         b.max_records = (uint32_t)(max_records > 0xFFFFFFFFull ? 0xFFFFFFFFull : max_records);
         b.tile0 = b.ntiles = b.sbase = b.cls = b.pad = 0;
         b.probed_dead = d_probed_dead;
+        b.dhash = nullptr;
         return true;
     }
 
@@ -258,7 +274,7 @@ struct DeviceState {
 // zero line count without a kernel). With more than kOverlay dead shards every batch is launched
 // on its own so that the deferred-probe list holds one batch at a time.
 template <int BLOCK, unsigned ABL>
-inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_t stream) {
+inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stream) {
     constexpr uint64_t T = (uint64_t)BLOCK * kLaneBytes;
     if (ds.wide() && in.nb > 1) {
         for (uint32_t i = 0; i < in.nb; ++i) {
@@ -320,9 +336,42 @@ inline int launch_route(const DeviceState &ds, const RouteParams &in, hipStream_
         grid_tiles = 8 * mx;
     }
     p.total_blocks = p.nb + grid_tiles;   // scanners first, then the tiles
+    // Two or more dead shards: probes past their first two picks are deferred to probe_defer_kernel,
+    // the record marked pending and the hash kept by record index (in the batch's hash array, or else
+    // in the context's scratch, grown outside stream capture; a launch that cannot have the scratch
+    // runs every probe in the route kernel).
+    p.defer = 0;
+    uint32_t max_recs = 0;
+    if (ds.dead >= 2 && ds.dead < ds.nds) {
+        uint64_t need = 0;
+        for (uint32_t j = 0; j < p.nb; ++j) {
+            if (!p.b[j].hashes) need += p.b[j].max_records;
+            max_recs = p.b[j].max_records > max_recs ? p.b[j].max_records : max_recs;
+        }
+        hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+        const bool capturing = hipStreamIsCapturing(stream, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+        if (need == 0 || need <= ds.defer_cap || (!capturing && ds.reserve_defer(need) == 0)) {
+            p.defer = 1;
+            uint64_t off = 0;
+            for (uint32_t j = 0; j < p.nb; ++j) {
+                if (p.b[j].hashes) {
+                    p.b[j].dhash = p.b[j].hashes;
+                } else {
+                    p.b[j].dhash = ds.d_defer + off;
+                    off += p.b[j].max_records;
+                }
+            }
+        }
+    }
     if (ds.wide() && hipMemsetAsync(&ds.d_ctl->pending, 0, sizeof(uint32_t), stream) != hipSuccess) return -EIO;
     hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     if (hipGetLastError() != hipSuccess) return -EIO;
+    if (p.defer) {   // the probes past their first two picks (probe_defer_kernel), grid y = batch
+        const uint32_t bx = (max_recs / 4u + 255u) / 256u;   // each lane looks at four records or so
+        hipLaunchKernelGGL(probe_defer_kernel, dim3(bx ? (bx < 512u ? bx : 512u) : 1u, p.nb), dim3(256), 0, stream,
+                           p);
+        if (hipGetLastError() != hipSuccess) return -EIO;
+    }
     if (ds.wide()) {
         ensure_dyn_lds((const void *)probe_wide_kernel, 160 * 1024);
         hipLaunchKernelGGL(probe_wide_kernel, dim3(256), dim3(64), (size_t)ds.nds * sizeof(uint16_t), stream, p);

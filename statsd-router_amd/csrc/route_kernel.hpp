@@ -60,7 +60,8 @@ constexpr int kOverlay = 16;                 // register overlay entries of the 
 constexpr int kNone = 0x1FFFF;               // "no colon" marker (above any tile position)
 constexpr int kSpinBudget = 1 << 14;         // polls before a missing predecessor is proxied
 constexpr uint32_t kFlagAgg = 1u, kFlagIncl = 2u;
-constexpr uint16_t kRoutePending = 0xFFFCu;  // internal: resolved by probe_wide_kernel
+constexpr uint16_t kRoutePending = 0xFFFCu;  // internal: resolved by probe_defer_kernel / probe_wide_kernel
+constexpr uint32_t kRouteDefer = 0xFFFBu;    // internal: probe_shard stopped after its first two picks
 constexpr uint64_t K = 65599ull;             // sdbm multiplier: (h<<6)+(h<<16)-h (sr-main.c:131)
 constexpr int kPowLo = 64, kPowHi = 24;     // K^i (i < 64) and K^(64 i) (i < 24: exponents below 1536)
 constexpr int kPowInv = 4;                   // K^-z (z < 4)
@@ -158,6 +159,7 @@ struct BatchDesc {
     uint32_t pad;
     uint64_t *probed_dead;   // may be null: bit k set = dead shard k was probed by some line
                              // (find_downstream zeroes its active buffer, sr-main.c:106)
+    uint64_t *dhash;         // RouteParams::defer: the hashes of deferred lines, by record index
 };
 
 struct RouteParams {
@@ -169,6 +171,8 @@ struct RouteParams {
     uint32_t pending_cap;
     uint32_t nwords_check;   // probed_dead_kernel: bitmap words checked for completion (0: never)
     uint32_t nwords;         // alive / probed-dead bitmap words
+    uint32_t defer;          // probes past their first two picks are deferred (probe_defer_kernel)
+    uint32_t pad_defer;
     Magic magic_n;           // for h % nds (fast path)
     const uint64_t *alive;   // bitmap
     const Magic *magic;      // [0..nds], index i -> divisor i
@@ -308,7 +312,7 @@ __device__ __forceinline__ uint32_t eq_mask16_dot(uint4 v, uint32_t pat) {
     return (lo + (hi << 8)) >> 7;
 }
 
-// '\n' and ':' masks (bit i = byte i) of a 16-byte piece, 8 VALU per dword for both patterns.
+// '\n' and ':' masks (bit i = byte i) of a 16-byte piece, 7 VALU per dword for both patterns.
 // For a pattern P with bit 7 clear, byte b == P iff bit 7 of b is clear and ((b & 0x7F) ^ P) + 0x7F
 // has bit 7 clear (the sum stays within the byte): the masked bytes and ~b's bit 7 are shared by
 // both patterns, the xor-add is one v_xad_u32, and the flag one v_bfi_b32.
@@ -322,16 +326,23 @@ __device__ __forceinline__ uint32_t xor_add(uint32_t a, uint32_t x, uint32_t y) 
     asm("v_xad_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(x), "v"(y));
     return r;
 }
+// ~a & ~b & c in one gfx950 v_bitop3_b32 (truth-table index a*4 + b*2 + c: only index 1 is set)
+__device__ __forceinline__ uint32_t nor_and(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x02" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
 __device__ __forceinline__ uint32_t nl_colon_mask16(uint4 v) {   // '\n' mask | ':' mask << 16
     const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
     uint32_t an = 0, cn = 0, ah = 0, ch = 0;
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
+        // 7 VALU per dword for both patterns: the masked bytes are shared, and the "bit 7 of the
+        // byte clear" term is folded into the flag's v_bitop3
         const uint32_t x = xs[d];
         const uint32_t x7 = x & 0x7F7F7F7Fu;
-        const uint32_t nx = not_and(x, 0x80808080u);
-        const uint32_t fn = not_and(xor_add(x7, 0x0A0A0A0Au, 0x7F7F7F7Fu), nx);
-        const uint32_t fc = not_and(xor_add(x7, 0x3A3A3A3Au, 0x7F7F7F7Fu), nx);
+        const uint32_t fn = nor_and(xor_add(x7, 0x0A0A0A0Au, 0x7F7F7F7Fu), x, 0x80808080u);
+        const uint32_t fc = nor_and(xor_add(x7, 0x3A3A3A3Au, 0x7F7F7F7Fu), x, 0x80808080u);
         const uint32_t w = (d & 1) ? 0x80402010u : 0x08040201u;
         if (d < 2) {
             an = __builtin_amdgcn_udot4(fn, w, an, false);
@@ -575,9 +586,13 @@ __device__ __forceinline__ void note_dead_wg(uint64_t *pd, unsigned long long *w
     note_dead(pd, k);
 }
 
+// DEFER (the route kernel, with dead shards): a line still unresolved after its first two picks
+// returns kRouteDefer; probe_defer_kernel runs its whole probe later, one lane per line (a wave
+// that runs the overlay loop below for one of its lines holds all its lanes for every step).
 template <bool MARK = false>
 __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark = nullptr,
-                                const uint32_t *pad_img = nullptr, unsigned long long *mark_wg = nullptr) {
+                                const uint32_t *pad_img = nullptr, unsigned long long *mark_wg = nullptr,
+                                bool defer = false) {
     const uint32_t n = p.nds;
     if (p.dead >= n) {                                    // includes N == 0
         if (MARK && n) note_all_dead(mark, n);
@@ -614,6 +629,7 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark
         }
         h = (h * 7 + 5) / 3;                                                              // :113
     }
+    if (defer && i > 0) return kRouteDefer;
     uint32_t ov[kOverlay];
     int nov = (o0 != 0xFFFFFFFFu) + (o1 != 0xFFFFFFFFu);
 #pragma unroll
@@ -750,6 +766,17 @@ __device__ __forceinline__ uint64_t sdbm_img(const S &sm, int a, int n, const ui
     for (; m < F; ++m) h = sdbm_dword_fast(h, p[m + 1]);
     if (rem) h = h * sm.kp_lo[rem] + sdbm_dword_fast(0, p[m + (m >= cross ? 1 : 0)] << (8 * (4 - rem)));
     return h;
+}
+
+// 32-bit LDS address of a __shared__ object, and a two-dword LDS store at immediate dword offsets
+// from one base register (the compiler rematerialises a base per store otherwise: 2 VALU each)
+__device__ __forceinline__ uint32_t lds_addr(const void *p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)p;
+}
+template <int O0, int O1>
+__device__ __forceinline__ void ds_write2_at(uint32_t base, uint32_t a, uint32_t b) {
+    asm volatile("ds_write2_b32 %0, %1, %2 offset0:%3 offset1:%4" ::"v"(base), "v"(a), "v"(b), "i"(O0), "i"(O1)
+                 : "memory");
 }
 
 // store / load one 16-byte chunk at image byte b (b % 16 == 0: never crosses a row)
@@ -1204,14 +1231,19 @@ __device__ __forceinline__ void tile_load(const RouteParams &p, SmemT<BLOCK> &sm
     stamp<ABL>(p, tid, g, 0);
     if (tid < kHalo / 16) img_put16(sm, tid * 16, in.hv);
     {
-        uint32_t *const row = &sm.img[(kHalo / 64 + tid) * 17];   // 17-dword rows: conflict-free per-lane rows
+        // 17-dword rows: conflict-free per-lane rows; eight two-dword stores from one base address
+        const uint32_t rb = lds_addr(&sm.img[(kHalo / 64 + tid) * 17]);
+        ds_write2_at<0, 1>(rb, in.v[0].x, in.v[0].y);
+        ds_write2_at<2, 3>(rb, in.v[0].z, in.v[0].w);
+        ds_write2_at<4, 5>(rb, in.v[1].x, in.v[1].y);
+        ds_write2_at<6, 7>(rb, in.v[1].z, in.v[1].w);
+        ds_write2_at<8, 9>(rb, in.v[2].x, in.v[2].y);
+        ds_write2_at<10, 11>(rb, in.v[2].z, in.v[2].w);
+        ds_write2_at<12, 13>(rb, in.v[3].x, in.v[3].y);
+        ds_write2_at<14, 15>(rb, in.v[3].z, in.v[3].w);
         uint32_t m[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            row[4 * k] = in.v[k].x;
-            row[4 * k + 1] = in.v[k].y;
-            row[4 * k + 2] = in.v[k].z;
-            row[4 * k + 3] = in.v[k].w;
             if (ABL & ABL_OLD_MASKS)
                 m[k] = eq_mask16_dot(in.v[k], 0x0A0A0A0Au) | (eq_mask16_dot(in.v[k], 0x3A3A3A3Au) << 16);
             else
@@ -1451,7 +1483,12 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 uint32_t route;
                 if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
                 else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
-                else route = probe_shard(h, p, nullptr, sm.img);                                   // :145
+                else route = probe_shard(h, p, nullptr, sm.img, nullptr, p.defer != 0);             // :145
+                // a probe past its first two picks goes to probe_defer_kernel: the record is marked
+                // pending and the hash kept by record index (no counter: same-address atomics from
+                // every wave serialise at the memory side)
+                const bool deferred = route == kRouteDefer;
+                if (deferred) route = kRoutePending;
                 sr_record r;
                 r.offset = (uint32_t)(T0 + s);
                 r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
@@ -1466,7 +1503,8 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 }
                 const uint32_t rec = base + (uint32_t)j;
                 if (rec < bd.max_records) {
-                    if (route == kRoutePending) {
+                    if (deferred) bd.dhash[rec] = h;
+                    if (route == kRoutePending && !deferred) {
                         const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
                         if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
                     }
@@ -1748,6 +1786,26 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     tile_lines<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
     if (tid == 0) arrive(p, blockIdx.x, ep0);
     stamp<ABL>(p, tid, g, 9);
+}
+
+// The probes the route kernel deferred (past their first two picks; DEFER in probe_shard): one lane
+// per deferred line, find_downstream (sr-main.c:86-117) from the line's hash with the 16-entry
+// register overlay; a line needing more goes on to probe_wide_kernel. Writes the record's route.
+__global__ __launch_bounds__(256) void probe_defer_kernel(RouteParams p) {
+    const uint32_t bi = blockIdx.y;   // grid y = batch
+    if (bi >= p.nb) return;
+    const BatchDesc &bd = p.b[bi];
+    const uint32_t n = (uint32_t)min(*bd.n_out, (uint64_t)bd.max_records);
+    for (uint32_t x = blockIdx.x * 256u + threadIdx.x; x < n; x += gridDim.x * 256u) {
+        if (bd.recs[x].route != kRoutePending) continue;
+        const uint64_t h = bd.dhash[x];
+        const uint32_t route = probe_shard(h, p);
+        if (route == kRoutePending) {   // more than kOverlay dead probes: probe_wide_kernel
+            const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
+            if (slot < p.pending_cap) p.pending[slot] = PendingLine{x, bi, h};
+        }
+        bd.recs[x].route = (uint16_t)route;
+    }
 }
 
 // Lines whose probe met more than kOverlay dead shards: run find_downstream (sr-main.c:86-117)

@@ -55,6 +55,9 @@ def run(exe, seconds, threads, rate, dgram, tmp, env=None, nblast=1):
         "offered_lines_per_s": round(sent["lines"] / sent["seconds"], 1),
         "offered_datagrams_per_s": round(sent["datagrams"] / sent["seconds"], 1),
         "delivered_lines": got["lines"], "delivered_lines_per_s": round(got["lines"] / span, 1),
+        # lines delivered per second of sending (the socket buffer and the pending buffers hold only a few
+        # datagrams past the blast; the sink's span also covers the last flush-timer tick)
+        "delivered_lines_per_blast_s": round(got["lines"] / sent["seconds"], 1),
         "delivered_fraction": round(got["lines"] / max(sent["lines"], 1), 4),
         "downstream_packets": got["datagrams"],
     }
