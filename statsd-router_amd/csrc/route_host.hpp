@@ -74,6 +74,7 @@ struct DeviceState {
     uint64_t *d_status = nullptr;
     uint64_t *d_bases = nullptr;
     PendingLine *d_pending = nullptr;
+    uint64_t *d_tile_pd = nullptr;       // per tile, its probed-dead words (RouteParams::mark)
     uint64_t *d_defer = nullptr;         // hashes of deferred probes by record index, for batches
     size_t defer_cap = 0;                // routed without a hash array (two or more dead shards)
     // lane layout of the route kernel (SR_LAYOUT_*): AUTO follows the segment statistics that
@@ -145,7 +146,9 @@ struct DeviceState {
         (void)hipFree(d_bases);
         (void)hipFree(d_pending);
         (void)hipFree(d_defer);
+        (void)hipFree(d_tile_pd);
         d_defer = nullptr;
+        d_tile_pd = nullptr;
         defer_cap = 0;
         if (h_layout) (void)hipHostFree(h_layout);
         h_layout = nullptr;
@@ -181,6 +184,10 @@ struct DeviceState {
                 return -ENOMEM;
             }
         }
+        if (dead && dead < nds && nds <= 64 * kAliveLds && !d_tile_pd &&
+            hipMalloc(&d_tile_pd, (size_t)(max_tiles ? max_tiles : 1) * nwords * sizeof(uint64_t)) != hipSuccess) {
+            d_tile_pd = nullptr;   // the launches replay the probes instead
+        }
         // the copy reads h_alive: complete it before the snapshot can change again
         return hipStreamSynchronize(stream) == hipSuccess ? 0 : -EIO;
     }
@@ -210,6 +217,7 @@ struct DeviceState {
         p.status = d_status;
         p.bases = d_bases;
         p.pending = d_pending;
+        p.tile_pd = d_tile_pd;
         p.dbg = nullptr;
         p.layout_out = d_layout;
         return p;
@@ -268,6 +276,10 @@ struct DeviceState {
     }
 
     bool wide() const { return dead > (uint32_t)kOverlay && dead < nds; }
+    // the probes note the dead shards they visit themselves (RouteParams::mark); otherwise a replay
+    // after the launch does (probed_dead_kernel), from the route kernel's hashes when it wrote them
+    bool marks_in_kernel() const { return dead && dead < nds && nds <= 64 * kAliveLds && d_tile_pd; }
+    bool replay_wants_hashes() const { return dead && dead < nds && !marks_in_kernel(); }
 };
 
 // Launch the route kernel over the batches of p (tile ranges assigned here; empty batches get a
@@ -341,6 +353,9 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
     // in the context's scratch, grown outside stream capture; a launch that cannot have the scratch
     // runs every probe in the route kernel).
     p.defer = 0;
+    // some shards dead (not all), at most 1024: the tiles note the dead shards their probes visit
+    // (MARK_LDS in route_kernel.hpp), probe_defer_kernel and probe_wide_kernel theirs; no replay
+    p.mark = (replay && ds.marks_in_kernel()) ? 1u : 0u;
     uint32_t max_recs = 0;
     if (ds.dead >= 2 && ds.dead < ds.nds) {
         uint64_t need = 0;
@@ -366,9 +381,11 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
     if (ds.wide() && hipMemsetAsync(&ds.d_ctl->pending, 0, sizeof(uint32_t), stream) != hipSuccess) return -EIO;
     hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     if (hipGetLastError() != hipSuccess) return -EIO;
-    if (p.defer) {   // the probes past their first two picks (probe_defer_kernel), grid y = batch
-        const uint32_t bx = (max_recs / 4u + 255u) / 256u;   // each lane looks at four records or so
-        hipLaunchKernelGGL(probe_defer_kernel, dim3(bx ? (bx < 512u ? bx : 512u) : 1u, p.nb), dim3(256), 0, stream,
+    if (p.defer || p.mark) {   // the probes past their first two picks and the OR of the tiles' probed-dead
+                               // slots (probe_defer_kernel), grid y = batch
+        // blocks past a batch's record count return at once; the rest loop over chunks of 4 waves
+        const uint32_t bx = p.defer ? (max_recs + 4u * kDeferChunk - 1u) / (4u * kDeferChunk) : 1u;
+        hipLaunchKernelGGL(probe_defer_kernel, dim3(bx ? (bx < 128u ? bx : 128u) : 1u, p.nb), dim3(256), 0, stream,
                            p);
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
@@ -377,7 +394,7 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
         hipLaunchKernelGGL(probe_wide_kernel, dim3(256), dim3(64), (size_t)ds.nds * sizeof(uint16_t), stream, p);
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
-    if (replay) {   // dead shards and a bitmap asked for: replay the probes (sr-main.c:106)
+    if (replay && !p.mark) {   // dead shards and a bitmap asked for: replay the probes (sr-main.c:106)
         p.nwords_check = ds.nwords <= kReplayCheckWords ? ds.nwords : 0u;
         hipLaunchKernelGGL(probed_dead_kernel, dim3(kReplayBlocks, p.nb), dim3(256), 0, stream, p);
         if (hipGetLastError() != hipSuccess) return -EIO;

@@ -172,7 +172,7 @@ struct RouteParams {
     uint32_t nwords_check;   // probed_dead_kernel: bitmap words checked for completion (0: never)
     uint32_t nwords;         // alive / probed-dead bitmap words
     uint32_t defer;          // probes past their first two picks are deferred (probe_defer_kernel)
-    uint32_t pad_defer;
+    uint32_t mark;           // tiles note the dead shards they probe (LDS, then one atomic per word)
     Magic magic_n;           // for h % nds (fast path)
     const uint64_t *alive;   // bitmap
     const Magic *magic;      // [0..nds], index i -> divisor i
@@ -181,6 +181,7 @@ struct RouteParams {
     uint64_t *status;        // per-tile '\n' count granules {epoch, flag, count} (written by the tile)
     uint64_t *bases;         // per-tile first-record granules {epoch, flag, base} (written by the scanner)
     PendingLine *pending;
+    uint64_t *tile_pd;       // mark: per tile (status granule index), its probed-dead words
     uint64_t *dbg;           // ABL_STAMPS builds only: 16 timestamp slots per tile
     uint32_t *layout_out;    // host-mapped {sequence, tiles weighed, tiles segmented} of the last
                              // KV_SEGMENTS launch (null: not published)
@@ -572,16 +573,26 @@ __device__ __forceinline__ uint32_t alive_pad_dword(const uint32_t *img, uint32_
     return img[(kAliveRow0 + (k >> 5)) * 17 + 16];
 }
 
-// note_dead with a workgroup's LDS copy of the bitmap in front (shards below 64 * kReplayCheckWords):
-// only the first lane of the workgroup to probe a dead shard touches the global word. The global
-// words are the hot addresses of a replay; same-address agent-scope traffic from every wave would
-// serialise at the memory side.
+// MARK_LDS (RouteParams::mark): the tile's probed-dead bits (sr-main.c:106) in the pad dwords of
+// rows kMarkRow0 .. (bit k in row kMarkRow0 + k / 32), stored in the tile's slot when it ends and
+// ORed per batch by probe_defer_kernel, instead of a replay after the launch. Atomic ORs per tile
+// serialise at the memory side: into the callers' words of 32 batches (two cache lines) +115 us per
+// C2 launch; into a line per batch, each followed by a wait before the block's arrival, +6 us.
+constexpr uint32_t kMarkRow0 = kAliveRow0 + 2 * kAliveLds;
+__device__ __forceinline__ void note_dead_lds(uint32_t *img, uint32_t k) {
+    atomicOr(&img[(kMarkRow0 + (k >> 5)) * 17 + 16], 1u << (k & 31));   // ds_or_b32, no return
+}
+
+// note_dead into a workgroup's LDS copy of the bitmap (shards below 64 * kReplayCheckWords); the
+// workgroup ORs its copy into the global words once per stride. The global words are the hot
+// addresses of a replay: same-address atomics, even one per workgroup and shard, serialise at the
+// memory side (measured: 74 us for 16 dead shards over 32 batches of C5).
 constexpr uint32_t kReplayCheckWords = 16;   // workgroup-local bitmap words (up to 1024 shards)
 __device__ __forceinline__ void note_dead_wg(uint64_t *pd, unsigned long long *wg, uint32_t k) {
-    if (wg && k < 64 * kReplayCheckWords) {
+    if (wg && k < 64 * kReplayCheckWords) {   // the workgroup pushes its copy to pd (probed_dead_kernel)
         const unsigned long long bit = 1ull << (k & 63);
-        if (wg[k >> 6] & bit) return;
-        if (atomicOr(&wg[k >> 6], bit) & bit) return;
+        if (!(wg[k >> 6] & bit)) atomicOr(&wg[k >> 6], bit);
+        return;
     }
     note_dead(pd, k);
 }
@@ -592,7 +603,7 @@ __device__ __forceinline__ void note_dead_wg(uint64_t *pd, unsigned long long *w
 template <bool MARK = false>
 __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark = nullptr,
                                 const uint32_t *pad_img = nullptr, unsigned long long *mark_wg = nullptr,
-                                bool defer = false) {
+                                bool defer = false, uint32_t *mark_lds = nullptr) {
     const uint32_t n = p.nds;
     if (p.dead >= n) {                                    // includes N == 0
         if (MARK && n) note_all_dead(mark, n);
@@ -622,6 +633,7 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark
         const uint32_t k = (o0 >> 16) == j ? (o0 & 0xFFFFu) : j;                         // :99
         if (alive_k(k)) return k;                                                         // :101-104
         if (MARK) note_dead_wg(mark, mark_wg, k);                                         // :106
+        if (mark_lds) note_dead_lds(mark_lds, k);
         if (j != i - 1) {                                                                 // :108-111
             const uint32_t v = (o0 >> 16) == i - 1 ? (o0 & 0xFFFFu) : i - 1;
             if (o0 == 0xFFFFFFFFu) o0 = (j << 16) | v;
@@ -642,6 +654,7 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark
             if ((ov[e] >> 16) == j) k = ov[e] & 0xFFFFu;
         if (alive_k(k)) return k;                                    // :101-104
         if (MARK) note_dead_wg(mark, mark_wg, k);                    // :106
+        if (mark_lds) note_dead_lds(mark_lds, k);
         if (j != i - 1) {                                            // :108-111
             uint32_t v = i - 1;
 #pragma unroll
@@ -1483,7 +1496,8 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 uint32_t route;
                 if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
                 else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
-                else route = probe_shard(h, p, nullptr, sm.img, nullptr, p.defer != 0);             // :145
+                else route = probe_shard(h, p, nullptr, sm.img, nullptr, p.defer != 0,
+                                         p.mark ? sm.img : nullptr);                                // :145
                 // a probe past its first two picks goes to probe_defer_kernel: the record is marked
                 // pending and the hash kept by record index (no counter: same-address atomics from
                 // every wave serialise at the memory side)
@@ -1724,8 +1738,8 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
         // the scanner is the latency-critical link of every tile's record base: its few
         // instructions go ahead of the co-resident tiles' VALU work
         __builtin_amdgcn_s_setprio(3);
-        // the batch's probed-dead bitmap starts empty (set after this launch by probe_wide_kernel and
-        // probed_dead_kernel, sr-main.c:106; with every shard alive it stays empty)
+        // the batch's probed-dead bitmap starts empty (set after this launch by probe_defer_kernel,
+        // probe_wide_kernel or probed_dead_kernel, sr-main.c:106; with every shard alive it stays empty)
         if (uint64_t *pd = p.b[blockIdx.x].probed_dead)
             for (uint32_t w = tid; w < p.nwords; w += BLOCK) pd[w] = 0ull;
         const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1779,32 +1793,99 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     if (p.dead && p.dead < p.nds && p.nds <= 64 * kAliveLds && tid >= (int)kAliveRow0 &&
         (uint32_t)tid < kAliveRow0 + 2 * ((p.nds + 63) / 64))   // the alive words (probe_shard)
         sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)p.alive)[tid - kAliveRow0];
+    if (p.mark && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
+        sm.img[(uint32_t)tid * 17 + 16] = 0u;
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
     uint64_t nlm, clm;
     uint32_t c_in;
     tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
     tile_lines<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
+    if (p.mark && p.b[bi].probed_dead) {   // MARK_LDS: the dead shards this tile's probes visited
+        wg_barrier();
+        if ((uint32_t)tid < p.nwords) {   // the tile's slot, ORed by probe_defer_kernel (no atomics)
+            const uint32_t lo = sm.img[(kMarkRow0 + 2 * (uint32_t)tid) * 17 + 16];
+            const uint32_t hi = sm.img[(kMarkRow0 + 2 * (uint32_t)tid + 1) * 17 + 16];
+            p.tile_pd[(size_t)(p.b[bi].sbase + t) * p.nwords + tid] = ((uint64_t)hi << 32) | lo;
+        }
+    }
     if (tid == 0) arrive(p, blockIdx.x, ep0);
     stamp<ABL>(p, tid, g, 9);
 }
 
-// The probes the route kernel deferred (past their first two picks; DEFER in probe_shard): one lane
-// per deferred line, find_downstream (sr-main.c:86-117) from the line's hash with the 16-entry
-// register overlay; a line needing more goes on to probe_wide_kernel. Writes the record's route.
+// After a route launch with dead shards. MARK_LDS: block 0 of each batch ORs the tiles' probed-dead
+// slots into the batch's bitmap (with the dead shards of its own probes, one atomic per word).
+// DEFER: the probes the route kernel deferred (past their first two picks; probe_shard):
+// find_downstream (sr-main.c:86-117) from the line's hash with the 16-entry register overlay; a line
+// needing more goes on to probe_wide_kernel. Writes the record's route. A few percent of the records
+// are deferred, so each wave first gathers the deferred record indices of a chunk of
+// kDeferChunk records into LDS (ballot + popcount, no atomics) and then probes them one per lane:
+// a wave runs the probe loop once per 64 deferred lines, not once per 64 records.
+// The reciprocals and alive words of probe_shard in the route kernel's pad-dword layout
+// (magic_from_pad, alive_pad_dword), for the kernels after it: a probe step then waits on LDS, not
+// on a dependent global load per step.
+constexpr uint32_t kProbePads = (kAliveRow0 + 2 * kAliveLds) * 17;
+__device__ __forceinline__ void load_probe_pads(const RouteParams &p, uint32_t *pads, uint32_t tid) {
+    if (tid < 4 * kMagicLds && (tid >> 2) < p.nds)
+        pads[tid * 17 + 16] = ((const uint32_t *)&p.magic[p.nds - (tid >> 2)])[tid & 3];
+    if (p.nds <= 64 * kAliveLds && tid >= kAliveRow0 && tid < kAliveRow0 + 2 * ((p.nds + 63) / 64))
+        pads[tid * 17 + 16] = ((const uint32_t *)p.alive)[tid - kAliveRow0];
+}
+
+constexpr uint32_t kDeferChunk = 256;   // records per wave and chunk (4 per lane)
 __global__ __launch_bounds__(256) void probe_defer_kernel(RouteParams p) {
+    __shared__ uint32_t pads[kProbePads];
+    __shared__ uint32_t list[4][kDeferChunk];
+    __shared__ unsigned long long wg[kReplayCheckWords];   // MARK: the block's probed-dead bits
     const uint32_t bi = blockIdx.y;   // grid y = batch
     if (bi >= p.nb) return;
     const BatchDesc &bd = p.b[bi];
     const uint32_t n = (uint32_t)min(*bd.n_out, (uint64_t)bd.max_records);
-    for (uint32_t x = blockIdx.x * 256u + threadIdx.x; x < n; x += gridDim.x * 256u) {
-        if (bd.recs[x].route != kRoutePending) continue;
-        const uint64_t h = bd.dhash[x];
-        const uint32_t route = probe_shard(h, p);
-        if (route == kRoutePending) {   // more than kOverlay dead probes: probe_wide_kernel
-            const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
-            if (slot < p.pending_cap) p.pending[slot] = PendingLine{x, bi, h};
+    if (blockIdx.x * 4u * kDeferChunk >= n) return;   // uniform over the block
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
+    load_probe_pads(p, pads, tid);
+    uint64_t *const mark = p.mark ? bd.probed_dead : nullptr;
+    if (tid < kReplayCheckWords) wg[tid] = 0ull;
+    __syncthreads();
+    if (mark && blockIdx.x == 0) {   // MARK_LDS: the OR of the batch's tile slots, into this block's copy
+        for (uint32_t q = 0; q < p.nwords; ++q) {
+            uint64_t v = 0;
+            for (uint32_t t = tid; t < bd.ntiles; t += 256u) v |= p.tile_pd[(size_t)(bd.sbase + t) * p.nwords + q];
+            if (v) atomicOr(&wg[q], (unsigned long long)v);
         }
-        bd.recs[x].route = (uint16_t)route;
+    }
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (uint32_t c = blockIdx.x * 4u + w; p.defer && c * kDeferChunk < n; c += gridDim.x * 4u) {
+        const uint32_t x0 = c * kDeferChunk + lane;
+        uint16_t r[kDeferChunk / 64];
+#pragma unroll
+        for (uint32_t it = 0; it < kDeferChunk / 64; ++it) {
+            const uint32_t x = x0 + 64u * it;
+            r[it] = x < n ? bd.recs[x].route : (uint16_t)0;
+        }
+        uint32_t cnt = 0;
+#pragma unroll
+        for (uint32_t it = 0; it < kDeferChunk / 64; ++it) {
+            const uint64_t m = __ballot(r[it] == kRoutePending);
+            if (r[it] == kRoutePending) list[w][cnt + __popcll(m & below)] = x0 + 64u * it;
+            cnt += __popcll(m);
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = lane; i < cnt; i += 64u) {
+            const uint32_t x = list[w][i];
+            const uint64_t h = bd.dhash[x];
+            const uint32_t route = mark ? probe_shard<true>(h, p, mark, pads, wg) : probe_shard(h, p, nullptr, pads);
+            if (route == kRoutePending) {   // more than kOverlay dead probes: probe_wide_kernel
+                const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
+                if (slot < p.pending_cap) p.pending[slot] = PendingLine{x, bi, h};
+            }
+            bd.recs[x].route = (uint16_t)route;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (mark) {   // the block's bits (p.mark: at most kAliveLds words), one atomic per nonzero word
+        __syncthreads();
+        if (tid < p.nwords && wg[tid])
+            __hip_atomic_fetch_or(mark + tid, (uint64_t)wg[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1862,30 +1943,41 @@ constexpr uint32_t kReplayBlocks = 32;
 
 __global__ __launch_bounds__(256) void probed_dead_kernel(RouteParams p) {
     __shared__ unsigned long long wg[kReplayCheckWords];
+    __shared__ unsigned long long pushed[kReplayCheckWords];
     __shared__ uint32_t complete;
+    __shared__ uint32_t pads[kProbePads];
     const uint32_t bi = blockIdx.y;
     if (bi >= p.nb) return;
     const BatchDesc &bd = p.b[bi];
     if (!bd.probed_dead) return;
     const uint32_t nw = p.nwords_check;   // 0: no workgroup copy, no completion test
-    if (threadIdx.x < kReplayCheckWords) wg[threadIdx.x] = 0ull;
+    if (threadIdx.x < kReplayCheckWords) wg[threadIdx.x] = pushed[threadIdx.x] = 0ull;
+    load_probe_pads(p, pads, threadIdx.x);
     const uint32_t n = (uint32_t)min(*bd.n_out, (uint64_t)bd.max_records);
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
+    // thread 0: OR the workgroup's new bits into the global words (one atomic per word that has
+    // any), and from the words' old values decide whether every dead shard is noted
+    auto push = [&]() {
+        bool all = nw != 0;
+        for (uint32_t w = 0; w < nw; ++w) {
+            const uint32_t hi = p.nds - 64 * w;
+            const uint64_t full = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
+            const uint64_t add = wg[w] & ~pushed[w];
+            uint64_t seen = wg[w] | p.alive[w];
+            if (add) {
+                pushed[w] |= add;
+                seen |= atomicOr((unsigned long long *)bd.probed_dead + w, (unsigned long long)add);
+            } else if ((seen & full) != full) {
+                seen |= __hip_atomic_load(bd.probed_dead + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            all = all && (seen & full) == full;
+        }
+        return all;
+    };
     for (uint32_t i0 = blockIdx.x * 256u; i0 < n; i0 += gridDim.x * 256u) {
         __syncthreads();
-        if (threadIdx.x == 0) {   // every dead shard already noted (by any workgroup): nothing left to add
-            bool all = nw != 0;
-            for (uint32_t w = 0; w < nw && all; ++w) {
-                const uint32_t hi = p.nds - 64 * w;
-                const uint64_t full = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
-                uint64_t seen = wg[w] | p.alive[w];
-                if ((seen & full) != full)
-                    seen |= __hip_atomic_load(bd.probed_dead + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                all = (seen & full) == full;
-            }
-            complete = all ? 1u : 0u;
-        }
+        if (threadIdx.x == 0) complete = push() ? 1u : 0u;
         __syncthreads();
         if (complete) return;
         const uint32_t i = i0 + threadIdx.x;
@@ -1893,15 +1985,7 @@ __global__ __launch_bounds__(256) void probed_dead_kernel(RouteParams p) {
         const sr_record r = bd.recs[i];
         if (r.route == SR_ROUTE_INVALID_LENGTH || r.route == SR_ROUTE_INVALID_FORMAT) continue;
         if (r.route == SR_ROUTE_ALL_DEAD) {   // every shard dead: the probe visited all of them
-            if (p.dead >= p.nds && p.nds) {
-                if (nw) {
-                    for (uint32_t w = 0; w < nw; ++w) {
-                        const uint32_t hi = p.nds - 64 * w;
-                        wg[w] = hi >= 64 ? ~0ull : ((1ull << hi) - 1ull);
-                    }
-                }
-                note_all_dead(bd.probed_dead, p.nds);
-            }
+            if (p.dead >= p.nds && p.nds) note_all_dead(bd.probed_dead, p.nds);
             continue;
         }
         // sdbm over the bytes before the first ':' (sr-main.c:120-134): the route kernel's own when it
@@ -1922,8 +2006,10 @@ __global__ __launch_bounds__(256) void probed_dead_kernel(RouteParams p) {
                 }
             }
         }
-        (void)probe_shard<true>(h, p, bd.probed_dead, nullptr, nw ? wg : nullptr);
+        (void)probe_shard<true>(h, p, bd.probed_dead, pads, nw ? wg : nullptr);
     }
+    __syncthreads();   // the last stride's bits
+    if (threadIdx.x == 0) (void)push();
 }
 
 }  // namespace srk

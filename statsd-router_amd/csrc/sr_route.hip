@@ -560,10 +560,11 @@ static int pack_submit(sr_ctx *c, int k, const uint8_t *bytes, size_t nbytes, co
         if (hipMemsetAsync(c->d_mcounts, 0, 4 * sizeof(uint64_t), c->stream) != hipSuccess) return -EIO;
     } else {
         if (hipMemcpyAsync(c->d_in, bytes, nbytes, hipMemcpyHostToDevice, c->stream) != hipSuccess) return -EIO;
-        // with dead shards the route kernel also writes the hashes: the probed-dead replay then
-        // reads 8 bytes per line instead of re-hashing the names (probed_dead_kernel)
+        // over 1024 shards with some dead the route kernel also writes the hashes: the probed-dead
+        // replay then reads 8 bytes per line instead of re-hashing the names (probed_dead_kernel);
+        // up to 1024 the probes note the dead shards themselves
         uint64_t *hashes = nullptr;
-        if (c->ds.dead) {
+        if (c->ds.replay_wants_hashes()) {
             if ((rc = grow((void **)&c->d_hash, &c->d_hash_cap, full, sizeof(uint64_t)))) return rc;
             hashes = c->d_hash;
         }
@@ -678,8 +679,8 @@ int sr_route_batch(sr_ctx *c, const uint8_t *bytes, size_t nbytes, sr_record *ou
         if (hipMalloc(&c->d_out, cap * sizeof(sr_record)) != hipSuccess) return -ENOMEM;
         c->d_out_cap = cap;
     }
-    // hashes: asked for, or (dead shards) for the probed-dead replay (probed_dead_kernel)
-    const bool want_hash = hashes || c->ds.dead;
+    // hashes: asked for, or for the probed-dead replay (probed_dead_kernel; over 1024 shards)
+    const bool want_hash = hashes || c->ds.replay_wants_hashes();
     if (want_hash && cap > c->d_hash_cap) {
         (void)hipFree(c->d_hash);
         c->d_hash = nullptr;
