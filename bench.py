@@ -330,7 +330,7 @@ def main(argv=None):
             result["e2e"] = e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M)
         if not args.no_pack:
             result["route_pack"] = pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev,
-                                            dead=sum(alive) < shards)
+                                            dead=sum(alive) < shards, alive=alive)
     router.close()
     del d_in, d_out
     torch.cuda.empty_cache()
@@ -594,71 +594,118 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8, exchange="
                      f"trip per step for the split sizes")}
 
 
-def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev, dead=False, reps=20):
+def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev, dead=False, reps=20,
+             alive=None):
     """The router's device data path: one route launch over M batches (the
     batches of M data threads), then the per-downstream MTU packing of all of them in one
     sr_pack_packets_many (sorted records + packet descriptors, each batch from its own pending
     bytes), captured in one graph and replayed back to back. Reported: lines/s through route +
-    packing, and the packing's own time."""
+    packing, and the packing's own time. Then the same with two contexts on two streams (two
+    router data threads sharing the GPU, as `threads_num` > 1 does): each replays its own
+    route + pack graph over its own M batches, and one context's packing runs beside the other's
+    route launch."""
     import torch
 
     max_lines = max(lines)
-    d_rec = torch.empty((M, max_lines), dtype=torch.int64, device=dev)
-    d_cnt = torch.zeros(M, dtype=torch.int64, device=dev)
     mp = pkg.max_packets(batch_bytes, shards)
-    d_srt = torch.empty((M, max_lines), dtype=torch.int64, device=dev)
-    d_pk = torch.empty((M, mp * 2), dtype=torch.int64, device=dev)
-    d_counts = torch.zeros((M, 3), dtype=torch.int64, device=dev)
-    d_fill = torch.zeros((M, shards), dtype=torch.int16, device=dev)
-    d_fout = torch.zeros((M, shards), dtype=torch.int16, device=dev)
-    # the probed-dead bitmap of every batch, as the router asks for it (sr-main.c:106; with every shard
-    # alive the route launch skips it)
-    d_pd = torch.zeros((M, max((shards + 63) // 64, 1)), dtype=torch.int64, device=dev)
-    # with dead shards the router has the route kernel write the hashes (the replay reads them)
-    d_h = torch.empty((M, max_lines), dtype=torch.int64, device=dev) if dead else None
     base = d_in.data_ptr()
+    nsets = max(1, len(sizes) // M)
 
-    def route():
-        router.route_device_many([(base + b * batch_bytes, sizes[b], d_rec[b].data_ptr(), max_lines,
-                                   d_h[b].data_ptr() if dead else None, d_cnt[b].data_ptr(), d_pd[b].data_ptr())
-                                  for b in range(M)])
+    class Thread:   # one data thread's device state: its context, stream, buffers and graphs
+        def __init__(self, rt, st, first):
+            self.rt, self.st, self.first = rt, st, first
+            self.rec = torch.empty((M, max_lines), dtype=torch.int64, device=dev)
+            self.cnt = torch.zeros(M, dtype=torch.int64, device=dev)
+            self.srt = torch.empty((M, max_lines), dtype=torch.int64, device=dev)
+            self.pk = torch.empty((M, mp * 2), dtype=torch.int64, device=dev)
+            self.counts = torch.zeros((M, 3), dtype=torch.int64, device=dev)
+            self.fill = torch.zeros((M, shards), dtype=torch.int16, device=dev)
+            self.fout = torch.zeros((M, shards), dtype=torch.int16, device=dev)
+            # the probed-dead bitmap of every batch, as the router asks for it (sr-main.c:106)
+            self.pd = torch.zeros((M, max((shards + 63) // 64, 1)), dtype=torch.int64, device=dev)
+            # with dead shards the router has the route kernel write the hashes (the replay reads them)
+            self.h = torch.empty((M, max_lines), dtype=torch.int64, device=dev) if dead else None
 
-    def pack():   # the batches of M data threads: independent pending bytes, one set of launches
-        router.pack_packets_many([(d_rec[b].data_ptr(), d_cnt[b].data_ptr(), max_lines, d_fill[b].data_ptr(),
-                                   d_pd[b].data_ptr(), d_srt[b].data_ptr(), d_pk[b].data_ptr(), mp,
-                                   d_counts[b].data_ptr(), d_fout[b].data_ptr()) for b in range(M)])
+        def route(self):
+            self.rt.route_device_many([(base + (self.first + b) * batch_bytes, sizes[self.first + b],
+                                        self.rec[b].data_ptr(), max_lines,
+                                        self.h[b].data_ptr() if dead else None, self.cnt[b].data_ptr(),
+                                        self.pd[b].data_ptr()) for b in range(M)])
 
-    with torch.cuda.stream(stream):
-        route()
-        pack()                                  # eager once: the packing scratch is allocated here
-        stream.synchronize()
-        g_all, g_route = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_all, stream=stream):
-            route()
-            pack()
-        with torch.cuda.graph(g_route, stream=stream):
-            route()
-        res = {}
-        for name, g in (("route_pack", g_all), ("route_only", g_route)):
+        def pack(self):   # the batches of M data threads: independent pending bytes, one set of launches
+            self.rt.pack_packets_many([(self.rec[b].data_ptr(), self.cnt[b].data_ptr(), max_lines,
+                                        self.fill[b].data_ptr(), self.pd[b].data_ptr(), self.srt[b].data_ptr(),
+                                        self.pk[b].data_ptr(), mp, self.counts[b].data_ptr(),
+                                        self.fout[b].data_ptr()) for b in range(M)])
+
+        def capture(self):
+            with torch.cuda.stream(self.st):
+                self.route()
+                self.pack()                                  # eager once: the packing scratch is allocated here
+                self.st.synchronize()
+                self.g_all, self.g_route = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(self.g_all, stream=self.st):
+                    self.route()
+                    self.pack()
+                with torch.cuda.graph(self.g_route, stream=self.st):
+                    self.route()
+
+    def replay(th, attr):   # a graph replays on the current stream: the thread's own
+        with torch.cuda.stream(th.st):
+            getattr(th, attr).replay()
+
+    def timed(threads, attr):
+        for th in threads:
             for _ in range(3):
-                g.replay()
-            a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record(stream)
-            for _ in range(reps):
-                g.replay()
-            z.record(stream)
-            z.synchronize()
-            res[name] = a.elapsed_time(z) / reps
-    packets = int(d_counts[:, 0].sum())
+                replay(th, attr)
+        torch.cuda.synchronize()
+        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(threads[0].st)
+        for th in threads[1:]:
+            th.st.wait_event(a)
+        for _ in range(reps):
+            for th in threads:
+                replay(th, attr)
+        for th in threads[1:]:
+            e = torch.cuda.Event()
+            e.record(th.st)
+            threads[0].st.wait_event(e)
+        z.record(threads[0].st)
+        z.synchronize()
+        return a.elapsed_time(z) / reps
+
+    t1 = Thread(router, stream, 0)
+    t1.capture()
+    res = {"route_pack": timed([t1], "g_all"), "route_only": timed([t1], "g_route")}
+    packets = int(t1.counts[:, 0].sum())
     tot_lines = sum(lines[:M])
-    return {"value": round(tot_lines / (res["route_pack"] * 1e-3) / 1e6, 3), "unit": "M metrics/s",
-            "ms_per_launch": round(res["route_pack"], 4), "route_only_ms": round(res["route_only"], 4),
-            "packing_ms": round(res["route_pack"] - res["route_only"], 4),
-            "packets_per_launch": packets,
-            "probed_dead_shards": int(sum(bin(int(w) & (2**64 - 1)).count("1") for w in d_pd[0].tolist())),
-            "note": (f"one route launch over {M} batches with their probed-dead bitmaps (sr-main.c:106, replayed when "
-                     f"a shard is dead) + one sr_pack_packets_many over them (regroup by downstream, next-fit 1450-byte "
-                     f"packets), one graph, {reps} replays")}
+    out = {"value": round(tot_lines / (res["route_pack"] * 1e-3) / 1e6, 3), "unit": "M metrics/s",
+           "ms_per_launch": round(res["route_pack"], 4), "route_only_ms": round(res["route_only"], 4),
+           "packing_ms": round(res["route_pack"] - res["route_only"], 4),
+           "packets_per_launch": packets,
+           "probed_dead_shards": int(sum(bin(int(w) & (2**64 - 1)).count("1") for w in t1.pd[0].tolist())),
+           "note": (f"one route launch over {M} batches with their probed-dead bitmaps (sr-main.c:106) + one "
+                    f"sr_pack_packets_many over them (regroup by downstream, next-fit 1450-byte packets), one "
+                    f"graph, {reps} replays")}
+    # two data threads on one GPU: a second context on its own stream over the next M batches
+    r2 = pkg.Router(shards, batch_bytes, device=dev.index)
+    try:
+        r2.set_alive(alive if alive is not None else [1] * shards)
+        s2 = torch.cuda.Stream(device=dev)
+        r2.set_stream(s2.cuda_stream)
+        t2 = Thread(r2, s2, M if nsets > 1 else 0)
+        t2.capture()
+        two = timed([t1, t2], "g_all")
+        lines2 = tot_lines + sum(lines[t2.first:t2.first + M])
+        out["two_threads"] = {
+            "value": round(lines2 / (two * 1e-3) / 1e6, 3), "unit": "M metrics/s",
+            "ms_per_round": round(two, 4), "packets_per_launch": [packets, int(t2.counts[:, 0].sum())],
+            "note": ("two router contexts (two data threads sharing the GPU), each with its own stream replaying "
+                     f"its own route + pack graph over its own {M} batches; the streams run concurrently, so one "
+                     "thread's packing overlaps the other's route launch; rate = both threads' lines / round")}
+    finally:
+        r2.close()
+    return out
 
 
 def e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M, groups=24):

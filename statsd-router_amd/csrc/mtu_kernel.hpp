@@ -41,7 +41,11 @@ namespace srk {
 constexpr int kMtuTile = 512;                    // records per sort tile (one wave)
 constexpr int kMtuChunk = 4096;                  // sorted lines per packing chunk (the larger size)
 constexpr int kMtuChunkSmall = 2048;             // ... the smaller: twice the chunks in flight, twice the chain
-constexpr int kMtuBlock = 256;                   // threads of the chunk kernels
+constexpr int kMtuBlock = 256;                   // threads of the emit kernel (and the prefix helper's default)
+#ifndef SR_MTU_TABLE_BLOCK
+#define SR_MTU_TABLE_BLOCK 256
+#endif
+constexpr int kMtuTableBlock = SR_MTU_TABLE_BLOCK;   // threads of the table kernel
 constexpr uint32_t kMtuMaxShards = 4096;
 constexpr int kMtuCap = (int)SR_DOWNSTREAM_BUF_SIZE;   // 1450: sr-types.h:30
 constexpr int kMtuWindow = kMtuCap / (int)SR_MIN_LINE_LENGTH + 1;   // a packet holds < 242 lines
@@ -78,6 +82,7 @@ struct MtuBatchArg {
 struct MtuLaunch {
     uint32_t nds, nb, tiles, chunks;   // shards; batches; record tiles and chunks of all batches
     uint32_t chunk_lines;              // lines per chunk of this launch (kMtuChunk or kMtuChunkSmall)
+    uint32_t hist_rep;                 // mtu_count: copies of each wave's histogram (a power of two)
     uint32_t *tile_counts;             // batch b at (nds + 1) * tile0: [(nds + 1) * ntiles], key-major
     uint32_t *keys;                    // [nb][2 * nds + 4]: key starts (nds + 2) | chunk firsts (nds + 1)
     uint32_t *chunk_shard;             // [chunks]
@@ -87,6 +92,8 @@ struct MtuLaunch {
     uint32_t *closed;                  // [nb][nds] packets closed per shard
     uint64_t *table;                   // [chunks][kMtuX]
     uint8_t *nx;                       // [chunks][kMtuChunk] next(i) - i per line (mtu_table -> mtu_emit)
+    uint16_t *slen;                    // [tiles * kMtuTile] the sorted lines' lengths (mtu_scatter -> chunk kernels)
+    uint32_t *gp;                      // [chunks][kMtuChunk] the chunks' length prefix sums (mtu_table -> mtu_emit)
     uint64_t *dbg;                     // SR_MTU_STAMPS developer builds only: 8 timestamps per chunk
     MtuBatchArg b[kMtuMaxBatches];
 };
@@ -109,11 +116,13 @@ struct MtuParams {
     uint32_t *chunk_shard;
     uint64_t *table;
     uint8_t *nx;
-    uint32_t *chunk_entry;
+    uint32_t *gp;
+    uint32_t *chunk_entry;    // incoming fill | first line over the cap from it << 16
     uint32_t *chunk_open;     // kMtuNone: the incoming packet began before the batch
     uint32_t *chunk_pk;
     uint32_t *closed;
     sr_record *sorted;
+    uint16_t *slen;           // lengths of the sorted records (2 B per line: what the chunk kernels read)
     sr_packet *packets;
     uint64_t max_packets;
     uint64_t *counts;
@@ -138,11 +147,13 @@ __device__ __forceinline__ MtuParams mtu_view(const MtuLaunch &L, uint32_t bi) {
     p.chunk_shard = L.chunk_shard + a.chunk0;
     p.table = L.table + (size_t)a.chunk0 * kMtuX;
     p.nx = L.nx + (size_t)a.chunk0 * kMtuChunk;
+    p.gp = L.gp + (size_t)a.chunk0 * kMtuChunk;
     p.chunk_entry = L.chunk_entry + a.chunk0;
     p.chunk_open = L.chunk_open + a.chunk0;
     p.chunk_pk = L.chunk_pk + a.chunk0;
     p.closed = L.closed + (size_t)bi * L.nds;
     p.sorted = a.sorted;
+    p.slen = L.slen + (size_t)a.tile0 * kMtuTile;
     p.packets = a.packets;
     p.max_packets = a.max_packets;
     p.counts = a.counts;
@@ -201,6 +212,9 @@ __device__ __forceinline__ void mtu_wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// The histogram is kept in hist_rep copies (key-major, copy = lane % hist_rep): LDS atomics from
+// the lanes of one instruction that hit one address serialise, and with few shards most of a
+// wave's 64 records share a handful of keys.
 __global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_count_kernel(MtuLaunch L) {
     extern __shared__ uint32_t lds_hist[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -208,20 +222,25 @@ __global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_count_kernel(MtuLaunch
     if (g >= L.tiles) return;
     const uint32_t bi = mtu_batch_of(L, g, [](const MtuBatchArg &a) { return a.tile0; });
     const MtuParams p = mtu_view(L, bi);
-    const uint32_t nk = p.nds + 1, t = g - L.b[bi].tile0;
-    uint32_t *hist = lds_hist + (size_t)wave * nk;
+    const uint32_t nk = p.nds + 1, t = g - L.b[bi].tile0, R = L.hist_rep;
+    uint32_t *hist = lds_hist + (size_t)wave * nk * R;
     const uint32_t n = mtu_lines(p), r0 = t * kMtuTile;
     sr_record r[kMtuPerLane];
     if (r0 < n) mtu_load_tile(p, r0, n, lane, r);
-    for (uint32_t k = lane; k < nk; k += 64) hist[k] = 0;
+    for (uint32_t k = lane; k < nk * R; k += 64) hist[k] = 0;
     mtu_wave_sync();
     if (r0 < n) {
+        const uint32_t cp = (uint32_t)lane & (R - 1u);
 #pragma unroll
         for (int k = 0; k < kMtuPerLane; ++k)
-            if (r0 + (uint32_t)(64 * k + lane) < n) atomicAdd(&hist[mtu_key(r[k], p.nds)], 1u);
+            if (r0 + (uint32_t)(64 * k + lane) < n) atomicAdd(&hist[mtu_key(r[k], p.nds) * R + cp], 1u);
     }
     mtu_wave_sync();
-    for (uint32_t k = lane; k < nk; k += 64) p.tile_counts[(size_t)k * p.ntiles + t] = hist[k];
+    for (uint32_t k = lane; k < nk; k += 64) {
+        uint32_t v = 0;
+        for (uint32_t q = 0; q < R; ++q) v += hist[k * R + q];
+        p.tile_counts[(size_t)k * p.ntiles + t] = v;
+    }
 }
 
 // One workgroup of 1024 threads: exclusive scan of the key-major table (position of (key, tile)
@@ -329,7 +348,9 @@ __global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_scatter_kernel(MtuLaun
             const uint64_t m = __ballot(mine);
             const uint32_t base = pos[k0];
             if (mine) {
-                p.sorted[base + (uint32_t)__popcll(m & lt)] = r;
+                const uint32_t q = base + (uint32_t)__popcll(m & lt);
+                p.sorted[q] = r;
+                p.slen[q] = r.length;
                 pend = false;
             }
             if (lane == leader) pos[k0] = base + (uint32_t)__popcll(m);
@@ -347,10 +368,12 @@ struct MtuTableSmem {
     uint32_t P[CH];      // inclusive prefix of the chunk's line lengths
     uint32_t ld[CH];     // last packet start reached from here << 16 | packets closed on the way
 };
-constexpr int kMtuHop = 16;   // packets per anchor of the emit walk
+#ifndef SR_MTU_HOP
+#define SR_MTU_HOP 16
+#endif
+constexpr int kMtuHop = SR_MTU_HOP;   // packets per anchor of the emit walk (a power of two)
 template <int CH>
 struct MtuEmitSmem {
-    uint32_t P[CH];
     alignas(16) uint8_t nx[CH];   // next(i) - i (1 .. kMtuWindow - 1), 0 = none in the chunk
     uint16_t J[CH];               // kMtuHop packet starts ahead on the chain (kMtuEnd: it ends first)
     uint16_t anchor[CH / kMtuHop + 2];
@@ -385,22 +408,22 @@ __device__ __forceinline__ uint32_t mtu_first_over(const uint32_t *P, uint32_t l
 // LDS prefix sums of the chunk's lengths. Wave w owns lines [1024 w, 1024 w + 1024), lane-
 // interleaved (line 1024 w + 64 k + lane): coalesced record loads, conflict-free LDS stores, the
 // running sum carried across the wave's 16 rows by DPP scans; one barrier for the wave offsets.
-template <int CH>
+template <int CH, int NT = kMtuBlock>
 __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuChunk &ck, uint32_t *P,
-                                                 uint32_t *wsum) {
-    constexpr int kMtuPer = CH / kMtuBlock;
+                                                 uint32_t *wsum, uint32_t *gP = nullptr) {
+    constexpr int kMtuPer = CH / NT;
     if (SR_MTU_SKIP & 16) {
-        for (uint32_t i = threadIdx.x; i < (uint32_t)CH; i += kMtuBlock) P[i] = 64u * (i + 1);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)CH; i += NT) P[i] = 64u * (i + 1);
         __syncthreads();
         return;
     }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t base = (uint32_t)wave * (CH / (kMtuBlock / 64)) + (uint32_t)lane;
+    const uint32_t base = (uint32_t)wave * (CH / (NT / 64)) + (uint32_t)lane;
     uint32_t v[kMtuPer];
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) {   // unconditional (clamped) loads: all 16 in flight together
         const uint32_t i = base + 64u * k;
-        const uint32_t len = p.sorted[ck.pos0 + min(i, ck.cnt - 1)].length;
+        const uint32_t len = p.slen[ck.pos0 + min(i, ck.cnt - 1)];
         v[k] = i < ck.cnt ? len : 0u;
     }
     uint32_t carry = 0;
@@ -415,6 +438,10 @@ __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuCh
     for (int w = 0; w < wave; ++w) add += wsum[w];
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) P[base + 64u * k] = v[k] + add;
+    if (gP) {   // the emit kernel's copy (coalesced rows; past the chunk's lines unused)
+#pragma unroll
+        for (int k = 0; k < kMtuPer; ++k) gP[base + 64u * k] = v[k] + add;
+    }
     __syncthreads();
 }
 
@@ -422,11 +449,11 @@ __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuCh
 // chunk), for lines tid + 256 k: a fixed 8-step search over the 256 lines after i (a packet holds
 // fewer than 242), the 16 searches of a thread independent, neighbouring lanes on neighbouring
 // words. f(i, next) stores the result.
-template <int CH, typename F>
+template <int CH, int NT, typename F>
 __device__ __forceinline__ void mtu_chunk_next(const uint32_t *P, uint32_t cnt, F f) {
-    constexpr int kMtuPer = CH / kMtuBlock;
+    constexpr int kMtuPer = CH / NT;
     if (SR_MTU_SKIP & 8) {
-        for (uint32_t i = threadIdx.x; i < cnt; i += kMtuBlock) f(i, i + 22 < cnt ? (uint16_t)(i + 22) : kMtuEnd);
+        for (uint32_t i = threadIdx.x; i < cnt; i += NT) f(i, i + 22 < cnt ? (uint16_t)(i + 22) : kMtuEnd);
         return;
     }
     // (every LDS read unconditional, at a clamped index: a read under a per-lane condition became
@@ -435,13 +462,44 @@ __device__ __forceinline__ void mtu_chunk_next(const uint32_t *P, uint32_t cnt, 
     uint32_t lo[kMtuPer], lim[kMtuPer];
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) {
-        const uint32_t i = threadIdx.x + (uint32_t)k * kMtuBlock;
+        const uint32_t i = threadIdx.x + (uint32_t)k * NT;
         lo[k] = i;   // P[i] <= lim: a line alone always fits
         const uint32_t pm = P[min(i ? i - 1 : 0u, cnt - 1)];
         lim[k] = pm * (uint32_t)(i != 0) + (uint32_t)kMtuCap;
     }
     // past the chunk the clamped read gives P[cnt - 1] = total, which is over lim unless no line
     // closes the packet (next = kMtuEnd below, lo unused): no bounds test, so no branch
+#if SR_MTU_NEXT_GUESS
+    // Row 0 by the search; every later row first tries row 0's offset (exact for lines of one
+    // length), and a wave searches a row only if one of its lanes missed.
+#pragma unroll
+    for (uint32_t step = 128; step; step >>= 1) {
+        const uint32_t t = lo[0] + step;
+        const uint32_t pt = P[min(t, cnt - 1)];
+        lo[0] = pt <= lim[0] ? t : lo[0];
+    }
+    const uint32_t d0 = lo[0] - threadIdx.x;
+    bool miss[kMtuPer];
+#pragma unroll
+    for (int k = 1; k < kMtuPer; ++k) {   // the guesses: two reads per row, all rows at once
+        const uint32_t g = min(lo[k] + d0, cnt - 1);
+        const uint32_t pg = P[g], pn = P[min(g + 1, cnt - 1)];
+        miss[k] = !(pg <= lim[k] && (g + 1 >= cnt || pn > lim[k]));
+        lo[k] = g;
+    }
+#pragma unroll
+    for (int k = 1; k < kMtuPer; ++k) {
+        if (__ballot(miss[k])) {
+            lo[k] = threadIdx.x + (uint32_t)k * NT;
+#pragma unroll
+            for (uint32_t step = 128; step; step >>= 1) {
+                const uint32_t t = lo[k] + step;
+                const uint32_t pt = P[min(t, cnt - 1)];
+                lo[k] = pt <= lim[k] ? t : lo[k];
+            }
+        }
+    }
+#else
 #pragma unroll
     for (uint32_t step = 128; step; step >>= 1) {
 #pragma unroll
@@ -451,17 +509,19 @@ __device__ __forceinline__ void mtu_chunk_next(const uint32_t *P, uint32_t cnt, 
             lo[k] = pt <= lim[k] ? t : lo[k];
         }
     }
+#endif
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) {
-        const uint32_t i = threadIdx.x + (uint32_t)k * kMtuBlock;
+        const uint32_t i = threadIdx.x + (uint32_t)k * NT;
         if (i < cnt) f(i, total <= lim[k] ? kMtuEnd : (uint16_t)(lo[k] + 1));
     }
 }
 
-// table[c][x] = (packets closed << 32) | (last packet start << 16, 0xFFFF = none) | fill after
-template <int CH>
-__global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
-    constexpr int kMtuPer = CH / kMtuBlock;
+// table[c][x] = (first line over the cap << 48) | (packets closed << 32) | (last packet start << 16,
+// 0xFFFF = none) | fill after (a chunk closes at most kMtuChunk + 1 packets: 16 bits)
+template <int CH, int NT = kMtuTableBlock>
+__global__ __launch_bounds__(NT) void mtu_table_kernel(MtuLaunch L) {
+    constexpr int kMtuPer = CH / NT;
     __shared__ MtuTableSmem<CH> sm;
     MtuChunk ck;
     const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.chunk0; });
@@ -470,14 +530,14 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
     if (!mtu_chunk_of(p, c, ck)) return;
     const int tid = threadIdx.x;
     mtu_stamp(L, blockIdx.x, 0);
-    mtu_chunk_prefix<CH>(p, ck, sm.P, sm.ld);
+    mtu_chunk_prefix<CH, NT>(p, ck, sm.P, sm.ld, p.gp + (size_t)c * kMtuChunk);
     mtu_stamp(L, blockIdx.x, 1);
     uint8_t *gnx = p.nx + (size_t)c * kMtuChunk;
-    mtu_chunk_next<CH>(sm.P, ck.cnt, [&](uint32_t i, uint16_t nxt) {
+    mtu_chunk_next<CH, NT>(sm.P, ck.cnt, [&](uint32_t i, uint16_t nxt) {
         sm.ld[i] = nxt == kMtuEnd ? i << 16 : ((uint32_t)nxt << 16) | 1u;
         if (!(SR_MTU_SKIP & 32)) gnx[i] = nxt == kMtuEnd ? 0 : (uint8_t)(nxt - i);   // for mtu_emit
     });
-    for (uint32_t i = ck.cnt + (uint32_t)tid; i < (uint32_t)CH; i += kMtuBlock) sm.ld[i] = i << 16;   // self loops
+    for (uint32_t i = ck.cnt + (uint32_t)tid; i < (uint32_t)CH; i += NT) sm.ld[i] = i << 16;   // self loops
     __syncthreads();
     mtu_stamp(L, blockIdx.x, 2);
     const uint32_t total = sm.P[ck.cnt - 1];
@@ -490,17 +550,17 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
     for (uint32_t span = 1; !(SR_MTU_SKIP & 1) && span < kb; span <<= 1) {
         uint32_t v[kMtuPer], w[kMtuPer];   // every line (past the chunk: self loops), loads first
 #pragma unroll
-        for (int k = 0; k < kMtuPer; ++k) v[k] = sm.ld[(uint32_t)tid + (uint32_t)k * kMtuBlock];
+        for (int k = 0; k < kMtuPer; ++k) v[k] = sm.ld[(uint32_t)tid + (uint32_t)k * NT];
 #pragma unroll
         for (int k = 0; k < kMtuPer; ++k) w[k] = sm.ld[v[k] >> 16];
 #pragma unroll
         for (int k = 0; k < kMtuPer; ++k)
-            sm.ld[(uint32_t)tid + (uint32_t)k * kMtuBlock] = (w[k] & 0xFFFF0000u) | ((v[k] + w[k]) & 0xFFFFu);
+            sm.ld[(uint32_t)tid + (uint32_t)k * NT] = (w[k] & 0xFFFF0000u) | ((v[k] + w[k]) & 0xFFFFu);
         __syncthreads();
     }
     mtu_stamp(L, blockIdx.x, 3);
     // incoming fills x0 .. x0 + per - 1 per thread: the first line over the cap moves down with x
-    constexpr uint32_t per = (kMtuX + kMtuBlock - 1) / kMtuBlock;
+    constexpr uint32_t per = (kMtuX + NT - 1) / NT;
     const uint32_t hi = min(ck.cnt, (uint32_t)kMtuWindow);
     uint64_t *row = p.table + (size_t)c * kMtuX;
     const uint32_t x0 = (uint32_t)tid * per;
@@ -519,7 +579,8 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_table_kernel(MtuLaunch L) {
                 while (j > 0 && sm.P[j - 1] > lim) --j;
             }
             const uint32_t v = sm.ld[j], l = v >> 16;
-            e = ((uint64_t)(1u + (v & 0xFFFFu)) << 32) | ((uint64_t)l << 16) | (total - (l ? sm.P[l - 1] : 0u));
+            e = ((uint64_t)j << 48) | ((uint64_t)(1u + (v & 0xFFFFu)) << 32) | ((uint64_t)l << 16) |
+                (total - (l ? sm.P[l - 1] : 0u));
         }
         row[x] = e;
     }
@@ -538,11 +599,11 @@ __global__ __launch_bounds__(1024) void mtu_chain_kernel(MtuLaunch L) {
         if (x > (uint32_t)kMtuCap) x = kMtuCap;
         const uint32_t c0 = p.chunk_first[s], c1 = min(p.chunk_first[s + 1], p.max_chunks);
         for (uint32_t c = c0; c < c1; ++c) {
-            p.chunk_entry[c] = x;
+            const uint64_t e = p.table[(size_t)c * kMtuX + x];
+            p.chunk_entry[c] = x | ((uint32_t)(e >> 48) << 16);
             p.chunk_open[c] = open;
             p.chunk_pk[c] = closed;   // shard-relative until the scan below
-            const uint64_t e = p.table[(size_t)c * kMtuX + x];
-            const uint32_t cl = (uint32_t)(e >> 32);
+            const uint32_t cl = (uint32_t)(e >> 32) & 0xFFFFu;
             if (cl) {
                 closed += cl;
                 open = p.key_start[s] + (c - c0) * p.chunk_lines + (uint32_t)((e >> 16) & 0xFFFFu);
@@ -583,9 +644,12 @@ __device__ __forceinline__ void mtu_put(const MtuParams &p, uint32_t k, uint32_t
 // The chunk's packet chain (the first line that does not fit the incoming packet, then next()):
 // four rounds of pointer doubling give every line the start kMtuHop packets ahead (J); one thread
 // walks the chain by those hops, leaving an anchor every kMtuHop packets; then every anchor's
-// thread walks its kMtuHop packets by next() and writes their descriptors (rank = 16 q + step).
+// thread walks its kMtuHop packets by next() (LDS), loads their prefix sums (the table kernel's
+// global copy, all loads in flight together) and writes their descriptors (rank = 16 q + step).
+// The chain's first line j comes with the chunk's incoming fill (mtu_chain, from the table): no
+// prefix sums in LDS, so that every chunk of a launch is resident at once.
 template <int CH>
-__global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuLaunch L) {
+__global__ __launch_bounds__(kMtuBlock, 8) void mtu_emit_kernel(MtuLaunch L) {   // 8 waves per SIMD: every chunk resident
     constexpr int kMtuPer = CH / kMtuBlock;
     __shared__ MtuEmitSmem<CH> sm;
     MtuChunk ck;
@@ -595,16 +659,10 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuLaunch L) {
     if (!mtu_chunk_of(p, c, ck)) return;
     mtu_stamp(L, blockIdx.x, 5);
     const int tid = threadIdx.x;
-    {   // next(i) - i as mtu_table stored it: 16 bytes per thread
-        const uint4 *src = reinterpret_cast<const uint4 *>(p.nx + (size_t)c * kMtuChunk);
-        const uint4 v = (uint32_t)tid * 16 < ck.cnt ? src[tid] : make_uint4(0, 0, 0, 0);
-        mtu_chunk_prefix<CH>(p, ck, sm.P, reinterpret_cast<uint32_t *>(sm.J));
-        if ((uint32_t)tid * 16 < (uint32_t)CH) reinterpret_cast<uint4 *>(sm.nx)[tid] = v;
-    }
-    __syncthreads();
-    mtu_stamp(L, blockIdx.x, 6);
-    const uint32_t x = p.chunk_entry[c], open = p.chunk_open[c], k0 = p.chunk_pk[c];
-    const uint32_t total = sm.P[ck.cnt - 1];
+    const uint32_t *gP = p.gp + (size_t)c * kMtuChunk;
+    const uint32_t xe = p.chunk_entry[c], open = p.chunk_open[c], k0 = p.chunk_pk[c];
+    const uint32_t x = xe & 0xFFFFu, j = xe >> 16;
+    const uint32_t total = gP[ck.cnt - 1];
     const uint32_t carry = open == kMtuNone ? x : 0u;        // pending bytes from before the batch
     const uint32_t start = open == kMtuNone ? p.key_start[ck.shard] : open;
     if (x + total <= (uint32_t)kMtuCap) {   // no line of the chunk closes a packet: the incoming one stays open
@@ -612,7 +670,16 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuLaunch L) {
             mtu_put(p, k0, start, ck.pos0 + ck.cnt - start, ck.shard, x - carry + total, carry, 1u);
         return;
     }
-    // J: next(i), then doubled four times (exact: all reads of a round before its writes)
+    if (tid == 0)   // the incoming packet closes before line j
+        mtu_put(p, k0, start, ck.pos0 + j - start, ck.shard, x - carry + (j ? gP[j - 1] : 0u), carry, 0u);
+    // next(i) - i as mtu_table stored it (16 bytes per thread), then J: next(i), doubled four times
+    // (exact: all reads of a round before its writes)
+    if ((uint32_t)tid * 16 < (uint32_t)CH)
+        reinterpret_cast<uint4 *>(sm.nx)[tid] = (uint32_t)tid * 16 < ck.cnt
+                                                   ? reinterpret_cast<const uint4 *>(p.nx + (size_t)c * kMtuChunk)[tid]
+                                                   : make_uint4(0, 0, 0, 0);
+    __syncthreads();
+    mtu_stamp(L, blockIdx.x, 6);
     uint16_t jv[kMtuPer];
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) {
@@ -633,10 +700,7 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuLaunch L) {
         for (int k = 0; k < kMtuPer; ++k) sm.J[(uint32_t)tid + (uint32_t)k * kMtuBlock] = jv[k];
         __syncthreads();
     }
-    const uint32_t j = mtu_first_over(sm.P, 0, min(ck.cnt, (uint32_t)kMtuWindow) - 1, (uint32_t)kMtuCap - x);
-    if (tid == 0) {
-        // the incoming packet closes before line j; anchors every kMtuHop packet starts from j
-        mtu_put(p, k0, start, ck.pos0 + j - start, ck.shard, x - carry + (j ? sm.P[j - 1] : 0u), carry, 0u);
+    if (tid == 0) {   // anchors every kMtuHop packet starts from j
         uint32_t n = 0;
         for (uint32_t a = j; !(SR_MTU_SKIP & 4);) {
             sm.anchor[n++] = (uint16_t)a;
@@ -649,17 +713,38 @@ __global__ __launch_bounds__(kMtuBlock) void mtu_emit_kernel(MtuLaunch L) {
     __syncthreads();
     const uint32_t na = sm.nanchor;
     for (uint32_t q = (uint32_t)tid; q < na; q += kMtuBlock) {
-        uint32_t a = sm.anchor[q], rank = q * kMtuHop;
-        for (int step = 0; step < kMtuHop; ++step, ++rank) {
-            const uint32_t d = sm.nx[a];
-            const bool is_open = d == 0;   // the last packet start: the packet stays pending
-            if (!is_open || ck.last) {     // else it continues into the next chunk
-                const uint32_t b = is_open ? ck.cnt : a + d;
-                mtu_put(p, k0 + 1 + rank, ck.pos0 + a, b - a, ck.shard, sm.P[b - 1] - (a ? sm.P[a - 1] : 0u), 0u,
-                        is_open ? 1u : 0u);
+        // the anchor's packets: starts and ends from next() in LDS, then every prefix sum they need
+        // loaded before the first descriptor store (a store waits for the loads issued before it)
+        // (consecutive packets: each starts where the one before it ends)
+        uint32_t bs[kMtuHop];
+        int ns = 0;
+        bool is_open = false;
+        const uint32_t a0 = sm.anchor[q];
+        uint32_t a = a0;
+#pragma unroll
+        for (int step = 0; step < kMtuHop; ++step) {
+            bs[step] = 1u;
+            if (ns == step && !is_open) {
+                const uint32_t d = sm.nx[a];
+                is_open = d == 0;            // the last packet start: the packet stays pending
+                bs[step] = is_open ? ck.cnt : a + d;
+                ns = step + ((!is_open || ck.last) ? 1 : 0);   // an open packet not in the last chunk continues
+                a += d;
             }
-            if (is_open) break;
-            a += d;
+        }
+        uint32_t pb[kMtuHop];
+        const uint32_t pl = gP[a0 ? a0 - 1u : 0u];   // unconditional (clamped) load
+        const uint32_t pa0 = a0 ? pl : 0u;
+#pragma unroll
+        for (int step = 0; step < kMtuHop; ++step) pb[step] = gP[bs[step] - 1u];   // all in flight together
+        uint32_t s0 = a0, p0 = pa0;
+#pragma unroll
+        for (int step = 0; step < kMtuHop; ++step) {
+            if (step < ns)
+                mtu_put(p, k0 + 1 + q * kMtuHop + (uint32_t)step, ck.pos0 + s0, bs[step] - s0, ck.shard, pb[step] - p0, 0u,
+                        (is_open && ck.last && step == ns - 1) ? 1u : 0u);   // the chain's open packet
+            s0 = bs[step];
+            p0 = pb[step];
         }
     }
     mtu_stamp(L, blockIdx.x, 7);
