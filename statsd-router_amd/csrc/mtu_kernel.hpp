@@ -82,7 +82,6 @@ struct MtuBatchArg {
 struct MtuLaunch {
     uint32_t nds, nb, tiles, chunks;   // shards; batches; record tiles and chunks of all batches
     uint32_t chunk_lines;              // lines per chunk of this launch (kMtuChunk or kMtuChunkSmall)
-    uint32_t hist_rep;                 // mtu_count: copies of each wave's histogram (a power of two)
     uint32_t *tile_counts;             // batch b at (nds + 1) * tile0: [(nds + 1) * ntiles], key-major
     uint32_t *keys;                    // [nb][2 * nds + 4]: key starts (nds + 2) | chunk firsts (nds + 1)
     uint32_t *chunk_shard;             // [chunks]
@@ -92,7 +91,6 @@ struct MtuLaunch {
     uint32_t *closed;                  // [nb][nds] packets closed per shard
     uint64_t *table;                   // [chunks][kMtuX]
     uint8_t *nx;                       // [chunks][kMtuChunk] next(i) - i per line (mtu_table -> mtu_emit)
-    uint16_t *slen;                    // [tiles * kMtuTile] the sorted lines' lengths (mtu_scatter -> chunk kernels)
     uint32_t *gp;                      // [chunks][kMtuChunk] the chunks' length prefix sums (mtu_table -> mtu_emit)
     uint64_t *dbg;                     // SR_MTU_STAMPS developer builds only: 8 timestamps per chunk
     MtuBatchArg b[kMtuMaxBatches];
@@ -122,7 +120,6 @@ struct MtuParams {
     uint32_t *chunk_pk;
     uint32_t *closed;
     sr_record *sorted;
-    uint16_t *slen;           // lengths of the sorted records (2 B per line: what the chunk kernels read)
     sr_packet *packets;
     uint64_t max_packets;
     uint64_t *counts;
@@ -153,7 +150,6 @@ __device__ __forceinline__ MtuParams mtu_view(const MtuLaunch &L, uint32_t bi) {
     p.chunk_pk = L.chunk_pk + a.chunk0;
     p.closed = L.closed + (size_t)bi * L.nds;
     p.sorted = a.sorted;
-    p.slen = L.slen + (size_t)a.tile0 * kMtuTile;
     p.packets = a.packets;
     p.max_packets = a.max_packets;
     p.counts = a.counts;
@@ -212,9 +208,6 @@ __device__ __forceinline__ void mtu_wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// The histogram is kept in hist_rep copies (key-major, copy = lane % hist_rep): LDS atomics from
-// the lanes of one instruction that hit one address serialise, and with few shards most of a
-// wave's 64 records share a handful of keys.
 __global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_count_kernel(MtuLaunch L) {
     extern __shared__ uint32_t lds_hist[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -222,25 +215,20 @@ __global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_count_kernel(MtuLaunch
     if (g >= L.tiles) return;
     const uint32_t bi = mtu_batch_of(L, g, [](const MtuBatchArg &a) { return a.tile0; });
     const MtuParams p = mtu_view(L, bi);
-    const uint32_t nk = p.nds + 1, t = g - L.b[bi].tile0, R = L.hist_rep;
-    uint32_t *hist = lds_hist + (size_t)wave * nk * R;
+    const uint32_t nk = p.nds + 1, t = g - L.b[bi].tile0;
+    uint32_t *hist = lds_hist + (size_t)wave * nk;
     const uint32_t n = mtu_lines(p), r0 = t * kMtuTile;
     sr_record r[kMtuPerLane];
     if (r0 < n) mtu_load_tile(p, r0, n, lane, r);
-    for (uint32_t k = lane; k < nk * R; k += 64) hist[k] = 0;
+    for (uint32_t k = lane; k < nk; k += 64) hist[k] = 0;
     mtu_wave_sync();
     if (r0 < n) {
-        const uint32_t cp = (uint32_t)lane & (R - 1u);
 #pragma unroll
         for (int k = 0; k < kMtuPerLane; ++k)
-            if (r0 + (uint32_t)(64 * k + lane) < n) atomicAdd(&hist[mtu_key(r[k], p.nds) * R + cp], 1u);
+            if (r0 + (uint32_t)(64 * k + lane) < n) atomicAdd(&hist[mtu_key(r[k], p.nds)], 1u);
     }
     mtu_wave_sync();
-    for (uint32_t k = lane; k < nk; k += 64) {
-        uint32_t v = 0;
-        for (uint32_t q = 0; q < R; ++q) v += hist[k * R + q];
-        p.tile_counts[(size_t)k * p.ntiles + t] = v;
-    }
+    for (uint32_t k = lane; k < nk; k += 64) p.tile_counts[(size_t)k * p.ntiles + t] = hist[k];
 }
 
 // One workgroup of 1024 threads: exclusive scan of the key-major table (position of (key, tile)
@@ -334,28 +322,26 @@ __global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_scatter_kernel(MtuLaun
 #pragma unroll
     for (int ck = 0; ck < kMtuPerLane; ++ck) keys[ck] = mtu_key(rr[ck], p.nds);
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the tile's records are in registers
+    const uint32_t kbits = nk > 1 ? 32u - (uint32_t)__clz(nk - 1u) : 0u;   // bits of the largest key
 #pragma unroll
     for (int ck = 0; ck < kMtuPerLane; ++ck) {
         const uint32_t i = r0 + (uint32_t)(64 * ck + lane);
-        bool pend = i < n;
-        const sr_record r = rr[ck];
+        const bool valid = i < n;
         const uint32_t key = keys[ck];
-        // stable in-wave ranks: one round per distinct key of the 64 records
-        for (uint64_t pm = __ballot(pend); pm; pm = __ballot(pend)) {
-            const int leader = __builtin_ctzll(pm);
-            const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)key, leader);
-            const bool mine = pend && key == k0;
-            const uint64_t m = __ballot(mine);
-            const uint32_t base = pos[k0];
-            if (mine) {
-                const uint32_t q = base + (uint32_t)__popcll(m & lt);
-                p.sorted[q] = r;
-                p.slen[q] = r.length;
-                pend = false;
-            }
-            if (lane == leader) pos[k0] = base + (uint32_t)__popcll(m);
-            mtu_wave_sync();
+        // stable in-wave ranks: the lanes holding my key, one ballot per key bit (not per distinct key)
+        uint64_t same = __ballot(valid);
+        for (uint32_t b = 0; b < kbits; ++b) {
+            const bool bit = ((key >> b) & 1u) != 0;
+            const uint64_t bm = __ballot(bit);
+            same &= bit ? bm : ~bm;
         }
+        const uint32_t base = pos[key];
+        mtu_wave_sync();   // every lane's read before a leader's write
+        if (valid) {
+            p.sorted[base + (uint32_t)__popcll(same & lt)] = rr[ck];
+            if (!(same & lt)) pos[key] = base + (uint32_t)__popcll(same);   // the key's first lane
+        }
+        mtu_wave_sync();
     }
 }
 
@@ -423,7 +409,7 @@ __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuCh
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) {   // unconditional (clamped) loads: all 16 in flight together
         const uint32_t i = base + 64u * k;
-        const uint32_t len = p.slen[ck.pos0 + min(i, ck.cnt - 1)];
+        const uint32_t len = p.sorted[ck.pos0 + min(i, ck.cnt - 1)].length;
         v[k] = i < ck.cnt ? len : 0u;
     }
     uint32_t carry = 0;

@@ -3,6 +3,10 @@
 # and a route+pack A/B of lib dirs. Usage (via gpurun): bash tools/r3_ab.sh <tag> [lib dirs...]
 tag=${1:-cur}; shift
 mkdir -p gpurun_out
+if [ -n "$R3_TESTS" ]; then
+  timeout -k 10 300 python -u -m pytest $R3_TESTS -x -q --timeout 120 --timeout-method thread > gpurun_out/${tag}_tests.log 2>&1 || { tail -30 gpurun_out/${tag}_tests.log; exit 1; }
+  tail -1 gpurun_out/${tag}_tests.log
+fi
 timeout -k 10 300 tools/ablate_route 64 quick > gpurun_out/abl_${tag}.json 2> gpurun_out/abl_${tag}.err || { cat gpurun_out/abl_${tag}.err; exit 1; }
 cat gpurun_out/abl_${tag}.json
 bash tools/pmc_ablate.sh gpurun_out/pmcabl_${tag} 64 quick || exit 1
