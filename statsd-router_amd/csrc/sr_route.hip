@@ -44,7 +44,6 @@ struct sr_ctx {
     uint32_t mtu_ntiles, mtu_chunks;
     uint32_t *d_mtu_tiles, *d_mtu_keys, *d_mtu_chunks;
     uint64_t *d_mtu_table;
-    uint16_t *d_mtu_len;   // the sorted lines' lengths, tiles * kMtuTile entries
     uint32_t *d_mtu_gp;    // the chunks' prefix sums, chunks * kMtuChunk entries
     // buffers of sr_route_pack_batch
     sr_record *d_sorted;
@@ -158,7 +157,6 @@ void sr_close(sr_ctx *c) {
     free_ptr(c->d_mtu_keys);
     free_ptr(c->d_mtu_chunks);
     free_ptr(c->d_mtu_table);
-    free_ptr(c->d_mtu_len);
     free_ptr(c->d_mtu_gp);
     free_ptr(c->d_sorted);
     free_ptr(c->d_packets);
@@ -344,12 +342,9 @@ static int mtu_reserve(sr_ctx *c, uint32_t tiles, uint32_t chunks, uint32_t nb) 
     const uint32_t nds = c->ds.nds;
     if (tiles > c->mtu_ntiles) {
         free_ptr(c->d_mtu_tiles);
-        free_ptr(c->d_mtu_len);
         c->d_mtu_tiles = nullptr;
-        c->d_mtu_len = nullptr;
         c->mtu_ntiles = 0;
         if (hipMalloc(&c->d_mtu_tiles, (size_t)(nds + 1) * tiles * sizeof(uint32_t)) != hipSuccess) return -ENOMEM;
-        if (hipMalloc(&c->d_mtu_len, (size_t)tiles * kMtuTile * sizeof(uint16_t)) != hipSuccess) return -ENOMEM;
         c->mtu_ntiles = tiles;
     }
     if (!c->d_mtu_keys) {   // keys and closed counts for the most batches a launch can hold
@@ -439,7 +434,6 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     L.chunk_pk = c->d_mtu_chunks + 3 * (size_t)chunks;
     L.table = c->d_mtu_table;
     L.nx = reinterpret_cast<uint8_t *>(c->d_mtu_table + (((size_t)c->mtu_chunks * kMtuX + 1) & ~(size_t)1));
-    L.slen = c->d_mtu_len;
     L.gp = c->d_mtu_gp;
 #ifdef SR_MTU_STAMPS   // developer timeline: 8 stamps per chunk, read back with sr_mtu_stamps
     static uint64_t *d_dbg = nullptr;
@@ -457,14 +451,11 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     L.dbg = nullptr;
 #endif
     const size_t sort_lds = (size_t)kMtuSortWaves * (nds + 1) * sizeof(uint32_t);
-    // count: histogram copies per wave, as many as fit 32 KiB per workgroup (up to 8)
-    L.hist_rep = 1;
-    while (L.hist_rep < 8 && sort_lds * L.hist_rep * 2 <= 32 * 1024) L.hist_rep *= 2;
     // up to 4 x 4097 counters: past the 64 KiB default
     ensure_dyn_lds((const void *)mtu_count_kernel, 96 * 1024);
     ensure_dyn_lds((const void *)mtu_scatter_kernel, 96 * 1024);
     const uint32_t sort_blocks = (tiles + kMtuSortWaves - 1) / kMtuSortWaves;
-    hipLaunchKernelGGL(mtu_count_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds * L.hist_rep, c->stream, L);
+    hipLaunchKernelGGL(mtu_count_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
     hipLaunchKernelGGL(mtu_scan_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
     hipLaunchKernelGGL(mtu_scatter_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
     if (ch == (uint32_t)kMtuChunk)
