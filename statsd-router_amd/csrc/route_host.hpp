@@ -4,6 +4,7 @@
 
 #include <errno.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -86,9 +87,15 @@ struct DeviceState {
     uint64_t launches = 0;
     uint32_t *h_layout = nullptr;    // pinned, device-mapped: {sequence, tiles weighed, tiles segmented}
     uint32_t *d_layout = nullptr;
+    // picks the route kernel makes before deferring a probe (RouteParams::picks) when the deferred
+    // probes run anyway (two or more dead shards): 1 (measured: C4 / C5 with 25 % dead 1-2 % faster
+    // than 2; with one dead shard nothing is deferred at 2 picks, and deferring a quarter of the
+    // lines cost C2 +30 %); SR_DEFER_PICKS=2 overrides
+    uint32_t defer_picks = 1;
 
     int init(size_t max_batch_bytes, uint32_t n_downstreams) {
         max_batch = max_batch_bytes;
+        if (const char *e = getenv("SR_DEFER_PICKS")) defer_picks = atoi(e) == 2 ? 2u : 1u;
         nds = n_downstreams;
         nwords = (n_downstreams + 63) / 64;
         // status granules for kMaxBatches batches of the smallest tile (256 threads, 16 KiB)
@@ -348,11 +355,12 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
         grid_tiles = 8 * mx;
     }
     p.total_blocks = p.nb + grid_tiles;   // scanners first, then the tiles
-    // Two or more dead shards: probes past their first two picks are deferred to probe_defer_kernel,
+    // Two or more dead shards: probes past their first pick are deferred to probe_defer_kernel,
     // the record marked pending and the hash kept by record index (in the batch's hash array, or else
     // in the context's scratch, grown outside stream capture; a launch that cannot have the scratch
     // runs every probe in the route kernel).
     p.defer = 0;
+    p.picks = ds.dead >= 2 ? ds.defer_picks : 2u;
     // some shards dead (not all), at most 1024: the tiles note the dead shards their probes visit
     // (MARK_LDS in route_kernel.hpp), probe_defer_kernel and probe_wide_kernel theirs; no replay
     p.mark = (replay && ds.marks_in_kernel()) ? 1u : 0u;

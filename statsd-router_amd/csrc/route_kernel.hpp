@@ -36,10 +36,12 @@
 //     lengths one lane per segment, lines packed back to back over the lanes, a line's hash the
 //     difference of an inclusive wave scan of segment hashes (route_host.hpp picks per launch).
 //   * Shard pick: h % N through a 64-bit magic reciprocal when every shard is alive; otherwise the
-//     reference's probe with a 16-entry register overlay of the permutation (the first reciprocals
-//     in LDS). Lines needing more than 16 dead probes are deferred to probe_wide_kernel (the probe
-//     on a full LDS permutation); the dead shards the probes visit (sr-main.c:106) come from
-//     probed_dead_kernel, a replay after the launch.
+//     reference's probe: its first two picks here (reciprocals and alive words in LDS pad dwords),
+//     a line needing a third deferred by record index to probe_defer_kernel (16-entry register
+//     overlay), and one needing more than 16 dead probes to probe_wide_kernel (the probe on a full
+//     LDS permutation). The dead shards the probes visit (sr-main.c:106) are noted by the probes
+//     themselves (LDS words per tile, ORed per batch by probe_defer_kernel); beyond 1024 shards
+//     probed_dead_kernel replays the probes from the hashes after the launch.
 //   * Every workgroup arrives on 8-way sharded counters without waiting; the last block waits for
 //     all arrivals and advances the context's epoch, so stale granules of earlier launches are never
 //     mistaken for current ones, with or without graph replay.
@@ -171,7 +173,8 @@ struct RouteParams {
     uint32_t pending_cap;
     uint32_t nwords_check;   // probed_dead_kernel: bitmap words checked for completion (0: never)
     uint32_t nwords;         // alive / probed-dead bitmap words
-    uint32_t defer;          // probes past their first two picks are deferred (probe_defer_kernel)
+    uint32_t defer;          // probes past their first `picks` picks are deferred (probe_defer_kernel)
+    uint32_t picks;          // with defer: picks the route kernel makes itself (1 or 2)
     uint32_t mark;           // tiles note the dead shards they probe (LDS, then one atomic per word)
     Magic magic_n;           // for h % nds (fast path)
     const uint64_t *alive;   // bitmap
@@ -546,10 +549,10 @@ __device__ __noinline__ void note_all_dead(uint64_t *pd, uint32_t n) {
 }
 
 // find_downstream (sr-main.c:86-117) for one line. Returns the shard, SR_ROUTE_ALL_DEAD, or
-// kRoutePending if more than kOverlay dead shards had to be probed. The dead shards the probe
-// visits (sr-main.c:106) are recorded by probed_dead_kernel, a replay after the launch: any extra
-// live value in this loop costs the route kernel a spill (measured: 9 % at C2, all alive).
-// MARK: when non-null, every dead shard visited is set in that bitmap (the replay's use).
+// kRoutePending if more than kOverlay dead shards had to be probed (kRouteDefer: stopped after its
+// first two picks, `defer`). The dead shards the probe visits (sr-main.c:106) go to mark_lds (the
+// route kernel's per-tile LDS words), to mark / mark_wg (probe_defer_kernel and the replay), or
+// nowhere: a global atomic per visit inside the route kernel's line loop cost 9 % at C2.
 // The route kernel keeps the divisors' reciprocals its probes need first, N .. N - kMagicLds + 1,
 // in the padding dword of LDS image rows (entry e, word w at row 4 e + w; the rows' padding is
 // never read as bytes), so that a probe step waits on LDS rather than on a global load (a global
@@ -628,7 +631,8 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark
     // shards nearly every line ends there, without scanning the 16-entry overlay.
     uint32_t o0 = 0xFFFFFFFFu, o1 = 0xFFFFFFFFu;   // (pos << 16) | value
     uint32_t i = n;
-    for (int it = 0; it < 2 && i > 0; ++it, --i) {
+    const int np = (defer && p.picks == 1) ? 1 : 2;
+    for (int it = 0; it < np && i > 0; ++it, --i) {
         const uint32_t j = mod_magic(h, magic_i(i), i);                                  // :98
         const uint32_t k = (o0 >> 16) == j ? (o0 & 0xFFFFu) : j;                         // :99
         if (alive_k(k)) return k;                                                         // :101-104
