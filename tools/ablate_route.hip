@@ -151,6 +151,8 @@ int main(int argc, char **argv) {
         if (quick) {
             put("m32", time_variant<256, ABL_NONE>(c, 1, reps, 32));
             put("m32_fake_base", time_variant<256, ABL_FAKE_BASE>(c, 1, reps, 32));
+            put("m32_early_base", time_variant<256, ABL_EARLY_BASE>(c, 1, reps, 32));
+            put("m32_no_mid_base", time_variant<256, ABL_NO_MID_BASE>(c, 1, reps, 32));
             put("m32_no_lookback", time_variant<256, ABL_NO_LOOKBACK>(c, 1, reps, 32));
             put("m32_no_hash", time_variant<256, ABL_NO_HASH>(c, 1, reps, 32));
             put("m32_no_prologue", time_variant<256, ABL_NO_PROLOGUE>(c, 1, reps, 32));
