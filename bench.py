@@ -82,6 +82,8 @@ def parse(argv=None):
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-pack", action="store_true", help="skip the route + MTU packing leg")
+    ap.add_argument("--pack-threads", type=int, default=2, choices=[1, 2],
+                    help="2: also time two data threads' route + pack graphs running concurrently")
     ap.add_argument("--layout", default="auto", choices=["auto", "uniform", "segments"],
                     help="route kernel lane layout (sr_set_layout; records identical either way)")
     ap.add_argument("--dry-ranks", action="store_true",
@@ -330,7 +332,7 @@ def main(argv=None):
             result["e2e"] = e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M)
         if not args.no_pack:
             result["route_pack"] = pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev,
-                                            dead=sum(alive) < shards, alive=alive)
+                                            dead=sum(alive) < shards, alive=alive, threads=args.pack_threads)
     router.close()
     del d_in, d_out
     torch.cuda.empty_cache()
@@ -595,7 +597,7 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8, exchange="
 
 
 def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev, dead=False, reps=20,
-             alive=None):
+             alive=None, threads=2):
     """The router's device data path: one route launch over M batches (the
     batches of M data threads), then the per-downstream MTU packing of all of them in one
     sr_pack_packets_many (sorted records + packet descriptors, each batch from its own pending
@@ -687,6 +689,8 @@ def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, de
            "note": (f"one route launch over {M} batches with their probed-dead bitmaps (sr-main.c:106) + one "
                     f"sr_pack_packets_many over them (regroup by downstream, next-fit 1450-byte packets), one "
                     f"graph, {reps} replays")}
+    if threads < 2:
+        return out
     # two data threads on one GPU: a second context on its own stream over the next M batches
     r2 = pkg.Router(shards, batch_bytes, device=dev.index)
     try:
