@@ -18,7 +18,7 @@
 //             find_downstream drops its buffer, sr-main.c:106).
 //
 // Kernels (all on the context's stream; one wave per record tile for the sort):
-//   mtu_count   per 512-record tile, a histogram of keys (shard, or N = unrouted) in LDS;
+//   mtu_count   per 1024-record tile, a histogram of keys (shard, or N = unrouted) in LDS;
 //   mtu_scan    one workgroup: exclusive scan of the key-major histogram table = the first sorted
 //               position of every (key, tile); shard line counts -> packing chunks;
 //   mtu_scatter per tile, stable in-wave ranks (one ballot per distinct key) -> sorted records;
@@ -38,7 +38,11 @@
 
 namespace srk {
 
-constexpr int kMtuTile = 512;                    // records per sort tile (one wave)
+#ifndef SR_MTU_TILE
+#define SR_MTU_TILE 1024
+#endif
+constexpr int kMtuTile = SR_MTU_TILE;            // records per sort tile (one wave; 1024: 16 loads in flight
+                                                 // per lane, count + scatter 2-3 % faster than 512)
 constexpr int kMtuChunk = 4096;                  // sorted lines per packing chunk (the larger size)
 constexpr int kMtuChunkSmall = 2048;             // ... the smaller: twice the chunks in flight, twice the chain
 constexpr int kMtuBlock = 256;                   // threads of the emit kernel (and the prefix helper's default)

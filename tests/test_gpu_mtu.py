@@ -279,3 +279,34 @@ def test_pack_packets_many_independent_batches(pkg, oracle, torch_stream):
         assert np.array_equal(srt, srt_o), b
         assert np.array_equal(pk.view(np.uint8), pk_o.view(np.uint8)), b
         assert d_fout[b].cpu().numpy().view(np.uint16).tolist() == fill_o.tolist(), b
+
+
+def test_route_pack_threads_share_the_gpu(pkg, oracle):
+    """Data threads share a GPU (the executable's threads_num > 1, bench.py's two_threads leg): four
+    contexts, each driven by its own host thread (ctypes drops the GIL), route and pack their own
+    streams of batches at the same time; every result equals the oracle's, so the contexts' device
+    state (look-back granules, epochs, packing scratch) does not cross."""
+    import threading
+
+    shapes = [([64], 4, 0.0), ([64, 256, 1024], 64, 0.25), ([256], 4, 0.25), ([6, 7, 13], 3, 0.0)]
+    errors = []
+
+    def worker(k):
+        lens, n, dead = shapes[k]
+        alive = _dead(n, dead, 100 + k)
+        try:
+            with pkg.Router(n, 1 << 20) as r:
+                r.set_alive(alive)
+                for b in range(6):
+                    s = pkg.gen_stream(1 << 20, lens, seed=0xBEEF + 97 * k + b, p_invalid=0.05)
+                    _check_pack(pkg, oracle, s.data, n, alive, [b * 37 % 1451] * n, r)
+        except Exception as e:   # reported from the main thread
+            errors.append((k, repr(e)))
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(len(shapes))]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not any(t.is_alive() for t in ts), "a data thread did not finish"
+    assert not errors, errors
