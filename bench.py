@@ -82,8 +82,9 @@ def parse(argv=None):
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-pack", action="store_true", help="skip the route + MTU packing leg")
-    ap.add_argument("--pack-threads", type=int, default=2, choices=[1, 2],
-                    help="2: also time two data threads' route + pack graphs running concurrently")
+    ap.add_argument("--pack-threads", type=int, default=1, choices=[1, 2],
+                    help="2: also time two data threads' route + pack graphs running concurrently (their "
+                         "route launches overlap: a rocprof mean over the run then mixes in stretched launches)")
     ap.add_argument("--layout", default="auto", choices=["auto", "uniform", "segments"],
                     help="route kernel lane layout (sr_set_layout; records identical either way)")
     ap.add_argument("--dry-ranks", action="store_true",
