@@ -43,8 +43,12 @@ namespace srk {
 #endif
 constexpr int kMtuTile = SR_MTU_TILE;            // records per sort tile (one wave; 1024: 16 loads in flight
                                                  // per lane, count + scatter 2-3 % faster than 512)
-constexpr int kMtuChunk = 4096;                  // sorted lines per packing chunk (the larger size)
-constexpr int kMtuChunkSmall = 2048;             // ... the smaller: twice the chunks in flight, twice the chain
+#ifndef SR_MTU_CHUNK
+#define SR_MTU_CHUNK 4096
+#endif
+constexpr int kMtuChunk = SR_MTU_CHUNK;          // sorted lines per packing chunk (the larger size)
+constexpr int kMtuChunkSmall = 2048;             // ... the smaller: more chunks in flight, a longer chain
+static_assert(kMtuChunk <= 8192 && kMtuChunk % kMtuChunkSmall == 0, "chunk entries hold line indices in 16 bits");
 constexpr int kMtuBlock = 256;                   // threads of the emit kernel (and the prefix helper's default)
 #ifndef SR_MTU_TABLE_BLOCK
 #define SR_MTU_TABLE_BLOCK 256
@@ -664,10 +668,11 @@ __global__ __launch_bounds__(kMtuBlock, 8) void mtu_emit_kernel(MtuLaunch L) {  
         mtu_put(p, k0, start, ck.pos0 + j - start, ck.shard, x - carry + (j ? gP[j - 1] : 0u), carry, 0u);
     // next(i) - i as mtu_table stored it (16 bytes per thread), then J: next(i), doubled four times
     // (exact: all reads of a round before its writes)
-    if ((uint32_t)tid * 16 < (uint32_t)CH)
-        reinterpret_cast<uint4 *>(sm.nx)[tid] = (uint32_t)tid * 16 < ck.cnt
-                                                   ? reinterpret_cast<const uint4 *>(p.nx + (size_t)c * kMtuChunk)[tid]
-                                                   : make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (uint32_t v = (uint32_t)tid; v * 16 < (uint32_t)CH; v += kMtuBlock)
+        reinterpret_cast<uint4 *>(sm.nx)[v] = v * 16 < ck.cnt
+                                                  ? reinterpret_cast<const uint4 *>(p.nx + (size_t)c * kMtuChunk)[v]
+                                                  : make_uint4(0, 0, 0, 0);
     __syncthreads();
     mtu_stamp(L, blockIdx.x, 6);
     uint16_t jv[kMtuPer];

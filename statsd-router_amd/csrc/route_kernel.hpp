@@ -1828,14 +1828,24 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
 // (magic_from_pad, alive_pad_dword), for the kernels after it: a probe step then waits on LDS, not
 // on a dependent global load per step.
 constexpr uint32_t kProbePads = (kAliveRow0 + 2 * kAliveLds) * 17;
+__device__ __forceinline__ bool probe_pad_value(const RouteParams &p, uint32_t tid, uint32_t &v) {
+    if (tid < 4 * kMagicLds && (tid >> 2) < p.nds) {
+        v = ((const uint32_t *)&p.magic[p.nds - (tid >> 2)])[tid & 3];
+        return true;
+    }
+    if (p.nds <= 64 * kAliveLds && tid >= kAliveRow0 && tid < kAliveRow0 + 2 * ((p.nds + 63) / 64)) {
+        v = ((const uint32_t *)p.alive)[tid - kAliveRow0];
+        return true;
+    }
+    return false;
+}
 __device__ __forceinline__ void load_probe_pads(const RouteParams &p, uint32_t *pads, uint32_t tid) {
-    if (tid < 4 * kMagicLds && (tid >> 2) < p.nds)
-        pads[tid * 17 + 16] = ((const uint32_t *)&p.magic[p.nds - (tid >> 2)])[tid & 3];
-    if (p.nds <= 64 * kAliveLds && tid >= kAliveRow0 && tid < kAliveRow0 + 2 * ((p.nds + 63) / 64))
-        pads[tid * 17 + 16] = ((const uint32_t *)p.alive)[tid - kAliveRow0];
+    uint32_t v;
+    if (probe_pad_value(p, tid, v)) pads[tid * 17 + 16] = v;
 }
 
 constexpr uint32_t kDeferChunk = 256;   // records per wave and chunk (4 per lane)
+constexpr uint32_t kDeferOrBlocks = 16; // blocks per batch that OR the tiles' probed-dead slots (MARK_LDS)
 __global__ __launch_bounds__(256) void probe_defer_kernel(RouteParams p) {
     __shared__ uint32_t pads[kProbePads];
     __shared__ uint32_t list[4][kDeferChunk];
@@ -1843,34 +1853,56 @@ __global__ __launch_bounds__(256) void probe_defer_kernel(RouteParams p) {
     const uint32_t bi = blockIdx.y;   // grid y = batch
     if (bi >= p.nb) return;
     const BatchDesc &bd = p.b[bi];
-    const uint32_t n = (uint32_t)min(*bd.n_out, (uint64_t)bd.max_records);
-    if (blockIdx.x * 4u * kDeferChunk >= n) return;   // uniform over the block
     const uint32_t tid = threadIdx.x, lane = tid & 63u, w = tid >> 6;
-    load_probe_pads(p, pads, tid);
     uint64_t *const mark = p.mark ? bd.probed_dead : nullptr;
+    // The block's independent loads first, so that their latencies overlap: the probe's pads, the
+    // record count, the routes of the wave's first chunk (bounded by the capacity; masked by the
+    // count below) and, in the first kDeferOrBlocks blocks, a slice of the tiles' probed-dead slots
+    // (word 0; MARK_LDS in the route kernel).
+    const uint32_t n = (uint32_t)min(*bd.n_out, (uint64_t)bd.max_records);
+    uint32_t pv = 0;
+    const bool has_pv = probe_pad_value(p, tid, pv);
+    const uint32_t nor = min(gridDim.x, kDeferOrBlocks);
+    uint64_t v0 = 0;
+    if (mark && blockIdx.x < nor)
+        for (uint32_t t = blockIdx.x * 256u + tid; t < bd.ntiles; t += nor * 256u)
+            v0 |= p.tile_pd[(size_t)(bd.sbase + t) * p.nwords];
+    if (blockIdx.x >= nor && blockIdx.x * 4u * kDeferChunk >= n) return;   // uniform over the block
+    const uint32_t x0 = (blockIdx.x * 4u + w) * kDeferChunk + lane;
+    uint16_t r0[kDeferChunk / 64];
+#pragma unroll
+    for (uint32_t it = 0; it < kDeferChunk / 64; ++it) {
+        const uint32_t x = x0 + 64u * it;
+        r0[it] = (p.defer && x < n) ? bd.recs[x].route : (uint16_t)0;
+    }
+    if (has_pv) pads[tid * 17 + 16] = pv;
     if (tid < kReplayCheckWords) wg[tid] = 0ull;
     __syncthreads();
-    if (mark && blockIdx.x == 0) {   // MARK_LDS: the OR of the batch's tile slots, into this block's copy
-        for (uint32_t q = 0; q < p.nwords; ++q) {
+    if (mark && blockIdx.x < nor) {   // MARK_LDS: the OR of the batch's tile slots, into this block's copy
+        if (v0) atomicOr(&wg[0], (unsigned long long)v0);
+        for (uint32_t q = 1; q < p.nwords; ++q) {
             uint64_t v = 0;
-            for (uint32_t t = tid; t < bd.ntiles; t += 256u) v |= p.tile_pd[(size_t)(bd.sbase + t) * p.nwords + q];
+            for (uint32_t t = blockIdx.x * 256u + tid; t < bd.ntiles; t += nor * 256u)
+                v |= p.tile_pd[(size_t)(bd.sbase + t) * p.nwords + q];
             if (v) atomicOr(&wg[q], (unsigned long long)v);
         }
     }
     const uint64_t below = (1ull << lane) - 1ull;
+    bool first = true;
     for (uint32_t c = blockIdx.x * 4u + w; p.defer && c * kDeferChunk < n; c += gridDim.x * 4u) {
-        const uint32_t x0 = c * kDeferChunk + lane;
+        const uint32_t xc = c * kDeferChunk + lane;
         uint16_t r[kDeferChunk / 64];
 #pragma unroll
         for (uint32_t it = 0; it < kDeferChunk / 64; ++it) {
-            const uint32_t x = x0 + 64u * it;
-            r[it] = x < n ? bd.recs[x].route : (uint16_t)0;
+            const uint32_t x = xc + 64u * it;
+            r[it] = x < n ? (first ? r0[it] : bd.recs[x].route) : (uint16_t)0;
         }
+        first = false;
         uint32_t cnt = 0;
 #pragma unroll
         for (uint32_t it = 0; it < kDeferChunk / 64; ++it) {
             const uint64_t m = __ballot(r[it] == kRoutePending);
-            if (r[it] == kRoutePending) list[w][cnt + __popcll(m & below)] = x0 + 64u * it;
+            if (r[it] == kRoutePending) list[w][cnt + __popcll(m & below)] = xc + 64u * it;
             cnt += __popcll(m);
         }
         __builtin_amdgcn_wave_barrier();
