@@ -85,11 +85,13 @@ def parse(argv=None):
     ap.add_argument("--pack-threads", type=int, default=1, choices=[1, 2],
                     help="2: also time two data threads' route + pack graphs running concurrently (their "
                          "route launches overlap: a rocprof mean over the run then mixes in stretched launches)")
-    ap.add_argument("--layout", default="auto", choices=["auto", "uniform", "segments"],
+    ap.add_argument("--layout", default="auto", choices=["auto", "uniform", "segments", "chunks"],
                     help="route kernel lane layout (sr_set_layout; records identical either way)")
     ap.add_argument("--dry-ranks", action="store_true",
                     help="each rank prints its RANK / LOCAL_RANK / WORLD_SIZE and exits (launcher test; no GPU)")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
+    # the PMC counter bytes of the dominant kernel (tools/pmc_summary.py): at the top of the tree so
+    # that it travels to the GPU box with the library it was measured on (profiles/ does not)
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "bench_traffic.json"))
     return ap.parse_args(argv)
 
 
@@ -194,7 +196,7 @@ def main(argv=None):
     router.set_alive(alive)
     router.set_stream(stream.cuda_stream)
     router.set_layout({"auto": pkg.SR_LAYOUT_AUTO, "uniform": pkg.SR_LAYOUT_UNIFORM,
-                       "segments": pkg.SR_LAYOUT_SEGMENTS}[args.layout])
+                       "segments": pkg.SR_LAYOUT_SEGMENTS, "chunks": pkg.SR_LAYOUT_CHUNKS}[args.layout])
     in_ptr, out_ptr, cnt_ptr = d_in.data_ptr(), d_out.data_ptr(), d_cnt.data_ptr()
 
     def launch(gi):
@@ -263,6 +265,7 @@ def main(argv=None):
         # the dominant kernel's achieved HBM rate: algorithmic bytes (the framed bytes, read once)
         # of the timed launches on this GPU over their GPU time
         achieved = steps_bytes / (region_ms * 1e-3) / 1e9
+        kernel_name = "route_chunk_kernel" if captured_layout == "chunks" else "route_kernel"
         traffic, traffic_src = None, None
         tj = args.traffic_json
         if tj and os.path.exists(tj):
@@ -271,12 +274,13 @@ def main(argv=None):
             # counter bytes of a rocprofv3 --pmc run (tools/pmc_summary.py) count only when they were
             # measured on this very build of the library and configuration
             lib_sha = hashlib.sha256(open(pkg.ROUTE_LIB, "rb").read()).hexdigest()
-            if tr.get("config") == args.config and tr.get("lib_sha256") == lib_sha:
+            if (tr.get("config") == args.config and tr.get("lib_sha256") == lib_sha
+                    and tr.get("kernel", kernel_name) == kernel_name):
                 traffic = tr.get("hbm_bytes_per_launch")
                 traffic_src = f"{os.path.relpath(tj, REPO)} (rocprofv3 --pmc of this build, lib sha256 {lib_sha[:12]})"
             else:
-                traffic_src = (f"{os.path.relpath(tj, REPO)} is for config {tr.get('config')} / lib "
-                               f"{str(tr.get('lib_sha256'))[:12]}, not this build: not reported")
+                traffic_src = (f"{os.path.relpath(tj, REPO)} is for config {tr.get('config')} / kernel "
+                               f"{tr.get('kernel')} / lib {str(tr.get('lib_sha256'))[:12]}, not this build: not reported")
         result = {
             "metric": "M metrics/s parsed+hashed, device-resident (GiB/s and HBM roofline alongside)",
             "value": round(total_lines / wall_max / 1e6, 3),
@@ -315,7 +319,7 @@ def main(argv=None):
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel": "route_kernel",
+                "kernel": kernel_name,
                 "read_ceiling": dict(ceiling, frac_of_ceiling=round(achieved / ceiling["achieved"], 4))
                 if ceiling.get("achieved") else ceiling,
                 "bytes_per_launch": steps_bytes / K,

@@ -48,6 +48,8 @@ struct sr_core {
     uint8_t *in[2];                          /* the two slots' framed datagrams                 */
     const uint8_t *in_flight_bytes;          /* the framed bytes of the batch in flight          */
     int in_flight;                           /* slot whose batch is on the GPU, or -1            */
+    unsigned fail_submit, submits;           /* fault injection (SR_CORE_FAIL_SUBMIT=k, tests):  */
+                                             /* the k-th sr_core_submit fails as a GPU error     */
     int host_fills;                          /* the host changed pending buffers since the last  */
                                              /* submission: upload them with the next one         */
     uint16_t *fill16;
@@ -154,6 +156,7 @@ int sr_core_open(sr_core **out, const sr_core_config *cfg, sr_core_emit_fn emit,
         return rc;
     }
     c->in_flight = -1;
+    if (getenv("SR_CORE_FAIL_SUBMIT")) c->fail_submit = (unsigned)strtoul(getenv("SR_CORE_FAIL_SUBMIT"), NULL, 0);
     c->host_fills = 1;
     c->msg_cap = 3 * SR_DATA_BUF_SIZE;
     c->ds = calloc(c->n, sizeof(ds_state));
@@ -299,14 +302,26 @@ int sr_core_submit(sr_core *c, int slot, size_t nbytes) {
     if (!c || slot < 0 || slot > 1 || nbytes > c->max_batch) return -EINVAL;
     if (c->in_flight == slot) return -EBUSY;
     if (nbytes == 0) return 0;
+    if (c->fail_submit && ++c->submits == c->fail_submit) return -EIO;   /* as a failed sr_route_pack_submit */
     int rc = submit(c, slot, c->in[slot], nbytes);
-    if (rc) return rc;
+    if (rc) return rc;   /* nothing submitted: sr_core_in_flight() is not `slot` */
     const int prev = c->in_flight;
     const uint8_t *prev_bytes = c->in_flight_bytes;
     c->in_flight = slot;
     c->in_flight_bytes = c->in[slot];
-    return prev >= 0 ? finish(c, prev, prev_bytes) : 0;
+    if (prev < 0) return 0;
+    if ((rc = finish(c, prev, prev_bytes)) == 0) return 0;
+    /* The previous batch failed, so its packets never reached the pending buffers the new batch's
+     * device-chained fills assume: take the new batch back and route it again from the host's fills
+     * (finish() set host_fills), so that host and device agree on every pending buffer. */
+    sr_pack_result r;
+    (void)sr_route_pack_result(c->ctx, slot, &r);
+    c->in_flight = -1;
+    if (submit(c, slot, c->in[slot], nbytes) == 0) c->in_flight = slot;
+    return rc;
 }
+
+int sr_core_in_flight(const sr_core *c) { return c ? c->in_flight : -EINVAL; }
 
 int sr_core_route(sr_core *c, const uint8_t *framed, size_t nbytes) {
     if (!c || (nbytes && !framed) || nbytes > c->max_batch) return -EINVAL;

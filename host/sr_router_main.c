@@ -123,9 +123,16 @@ static void submit_batch(data_thread *d) {
     refresh_alive(d);
     int rc = sr_core_submit(d->core, d->slot, d->len);
     if (rc) sr_log(SR_ERROR, "%s: sr_core_submit() failed %s", "udp_read_cb", strerror(-rc));
+    d->len = 0;
+    if (sr_core_in_flight(d->core) != d->slot) {
+        /* the batch was not taken (its lines are lost, as the ERROR says): complete the one in
+         * flight and keep filling this slot, which no GPU work reads */
+        int rc2 = sr_core_drain(d->core);
+        if (rc2) sr_log(SR_ERROR, "%s: sr_core_drain() failed %s", "udp_read_cb", strerror(-rc2));
+        return;
+    }
     d->slot ^= 1;
     d->batch = sr_core_slot_buffer(d->core, d->slot, &d->cap);
-    d->len = 0;
 }
 
 static void drain(data_thread *d) {

@@ -106,6 +106,7 @@ int sr_set_stream(sr_ctx *ctx, void *stream);
 #define SR_LAYOUT_AUTO 0
 #define SR_LAYOUT_UNIFORM 1
 #define SR_LAYOUT_SEGMENTS 2
+#define SR_LAYOUT_CHUNKS 3
 int sr_set_layout(sr_ctx *ctx, int layout);
 
 /* The layout the last route launch of the context used (SR_LAYOUT_UNIFORM or SR_LAYOUT_SEGMENTS;

@@ -87,6 +87,12 @@ uint8_t *sr_core_slot_buffer(sr_core *core, int slot, size_t *capacity);
 int sr_core_submit(sr_core *core, int slot, size_t nbytes);
 int sr_core_drain(sr_core *core);
 
+/* The slot whose batch is on the GPU (0 or 1), -1 if none, -EINVAL. After a failed sr_core_submit
+ * it tells the caller whether the new batch was taken (the call can also fail after submitting it,
+ * when completing the previous batch failed): a caller that refills the other slot only when
+ * sr_core_in_flight() == slot never overwrites a batch still in flight. */
+int sr_core_in_flight(const sr_core *core);
+
 /* ds_flush_timer_cb (sr-main.c:194-204): flush every non-empty pending buffer. */
 int sr_core_flush_timer(sr_core *core);
 

@@ -54,9 +54,9 @@ ABI_FUNCTIONS = (
     "sr_exchange_plan", "sr_exchange_run", "sr_exchange_rebase", "sr_route_pack_submit", "sr_route_pack_result",
 )
 SR_MAX_PACK_DOWNSTREAMS = 4096
-SR_LAYOUT_AUTO, SR_LAYOUT_UNIFORM, SR_LAYOUT_SEGMENTS = 0, 1, 2
+SR_LAYOUT_AUTO, SR_LAYOUT_UNIFORM, SR_LAYOUT_SEGMENTS, SR_LAYOUT_CHUNKS = 0, 1, 2, 3
 SR_COMM_ID_BYTES = 128
-LAYOUT_NAMES = {0: "none", 1: "uniform", 2: "segments"}
+LAYOUT_NAMES = {0: "none", 1: "uniform", 2: "segments", 3: "chunks"}
 PACKET_DTYPE = np.dtype([("first", "<u4"), ("nlines", "<u2"), ("shard", "<u2"), ("length", "<u2"),
                          ("carry", "<u2"), ("open", "<u4")])
 assert PACKET_DTYPE.itemsize == 16
@@ -334,12 +334,13 @@ class Router:
         self.stream_handle = int(stream_handle or 0)
 
     def set_layout(self, layout: int) -> None:
-        """sr_set_layout: SR_LAYOUT_AUTO (default), SR_LAYOUT_UNIFORM or SR_LAYOUT_SEGMENTS (the
-        route kernel's lane layout; records are identical either way)."""
+        """sr_set_layout: SR_LAYOUT_AUTO (default), SR_LAYOUT_UNIFORM, SR_LAYOUT_SEGMENTS or
+        SR_LAYOUT_CHUNKS (the route kernel's lane layout; records are identical either way)."""
         _check(self._lib.sr_set_layout(self._h, int(layout)), "sr_set_layout")
 
     def last_layout(self) -> int:
-        """sr_last_layout: the lane layout of the context's last route launch (1 uniform, 2 segments)."""
+        """sr_last_layout: the lane layout of the context's last route launch (1 uniform, 2 segments,
+        3 chunks)."""
         return _check(self._lib.sr_last_layout(self._h), "sr_last_layout")
 
     def route(self, data: bytes | np.ndarray, max_records: int | None = None, want_hashes: bool = False):

@@ -52,6 +52,7 @@ def router_lib() -> ctypes.CDLL:
         L.sr_core_slot_buffer.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]
         L.sr_core_submit.restype, L.sr_core_submit.argtypes = ctypes.c_int, [vp, ctypes.c_int, ctypes.c_size_t]
         L.sr_core_drain.restype, L.sr_core_drain.argtypes = ctypes.c_int, [vp]
+        L.sr_core_in_flight.restype, L.sr_core_in_flight.argtypes = ctypes.c_int, [vp]
         L.sr_core_flush_timer.restype, L.sr_core_flush_timer.argtypes = ctypes.c_int, [vp]
         L.sr_core_ping.restype, L.sr_core_ping.argtypes = ctypes.c_int, [vp]
         L.sr_core_state.restype = ctypes.c_int
@@ -136,6 +137,10 @@ class Core:
         ctypes.memmove(p, bytes(framed), len(framed))
         _check(self._L.sr_core_submit(self._h, slot, len(framed)), "sr_core_submit")
         self._slot = slot ^ 1
+
+    def in_flight(self) -> int:
+        """sr_core_in_flight: the slot whose batch is on the GPU, or -1."""
+        return self._L.sr_core_in_flight(self._h)
 
     def drain(self) -> None:
         _check(self._L.sr_core_drain(self._h), "sr_core_drain")

@@ -137,16 +137,20 @@ inline int exchange_run(const sr_transport &t, int world, int rank, const uint64
     if ((tot[1] && !packed) || (tot[0] && !packed_recs) || (tot[3] && !recv_bytes) || (tot[2] && !recv_recs))
         return -EINVAL;
     if ((rc = t.group_start(t.user))) return rc;
+    // Every operation is posted even after one fails, so that the peers' matching operations can
+    // complete and no peer waits forever inside the group; the first error is returned. A transport
+    // error still leaves the communicator unusable: the caller destroys it (sr_comm_close).
     int bad = 0;
-    for (int q = 0; q < world && !bad; ++q) {
+    auto post = [&bad](int r) {
+        if (r && !bad) bad = r;
+    };
+    for (int q = 0; q < world; ++q) {
         if (q == rank) continue;
         const sr_exchange_peer &e = peers[q];
-        if (e.send_bytes) bad = t.send(t.user, packed + e.send_byte0, e.send_bytes, q, 0);
-        if (!bad && e.recv_bytes) bad = t.recv(t.user, recv_bytes + e.recv_byte0, e.recv_bytes, q, 0);
-        if (!bad && e.send_lines)
-            bad = t.send(t.user, packed_recs + e.send_line0, e.send_lines * sizeof(sr_record), q, 1);
-        if (!bad && e.recv_lines)
-            bad = t.recv(t.user, recv_recs + e.recv_line0, e.recv_lines * sizeof(sr_record), q, 1);
+        if (e.send_bytes) post(t.send(t.user, packed + e.send_byte0, e.send_bytes, q, 0));
+        if (e.recv_bytes) post(t.recv(t.user, recv_bytes + e.recv_byte0, e.recv_bytes, q, 0));
+        if (e.send_lines) post(t.send(t.user, packed_recs + e.send_line0, e.send_lines * sizeof(sr_record), q, 1));
+        if (e.recv_lines) post(t.recv(t.user, recv_recs + e.recv_line0, e.recv_lines * sizeof(sr_record), q, 1));
     }
     rc = t.group_end(t.user);   // always closed, also after a failed post
     if (bad) return bad;

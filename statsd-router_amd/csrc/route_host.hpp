@@ -12,7 +12,7 @@
 #include <utility>
 #include <vector>
 
-#include "route_kernel.hpp"
+#include "chunk_kernel.hpp"
 
 namespace srk {
 
@@ -71,6 +71,9 @@ struct DeviceState {
     uint64_t *d_alive = nullptr;
     Magic *d_magic = nullptr;
     uint64_t *d_kpow = nullptr;
+    uint64_t *d_cpow = nullptr;          // route_chunk_kernel's power tables (kCpowEntries)
+    uint64_t *d_tail = nullptr;          // route_chunk_kernel's tail granules, 4 per tile
+    uint32_t lb_spin = 1u << 16;         // its look-back polls before computing a line itself
     Control *d_ctl = nullptr;
     uint64_t *d_status = nullptr;
     uint64_t *d_bases = nullptr;
@@ -105,6 +108,14 @@ struct DeviceState {
         if (hipMalloc(&d_alive, (nwords ? nwords : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&d_magic, (n_downstreams + 1) * sizeof(Magic)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&d_kpow, (kPowLo + kPowHi + kPowInv) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+        if (hipMalloc(&d_cpow, kCpowEntries * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+        if (hipMalloc(&d_tail, (max_tiles ? max_tiles : 1) * 4 * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
+        if (hipMemset(d_tail, 0, (max_tiles ? max_tiles : 1) * 4 * sizeof(uint64_t)) != hipSuccess) return -EIO;
+        if (const char *e = getenv("SR_LB_SPIN")) lb_spin = (uint32_t)strtoul(e, nullptr, 0);
+        if (const char *e = getenv("SR_LAYOUT")) {   // the context's initial layout (tests run every layout)
+            const int v = atoi(e);
+            if (v >= SR_LAYOUT_AUTO && v <= SR_LAYOUT_CHUNKS) layout_mode = v;
+        }
         if (hipMalloc(&d_ctl, sizeof(Control)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&d_status, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&d_bases, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
@@ -136,6 +147,14 @@ struct DeviceState {
         for (int z = 0; z < kPowInv; ++z) kp[kPowLo + kPowHi + z] = ipow(kKinv, (unsigned)z);
         if (hipMemcpy(d_kpow, kp.data(), kp.size() * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess)
             return -EIO;
+        std::vector<uint64_t> cp(kCpowEntries);
+        for (int z = 0; z < kCinv; ++z) cp[z] = ipow(kKinv, (unsigned)z);
+        for (int l = 0; l < 256; ++l) {
+            cp[kCinv + l] = ipow(K, 64u * (255u - (unsigned)l));
+            cp[kCinv + 256 + l] = ipow(kKinv, 64u * (255u - (unsigned)l));
+        }
+        if (hipMemcpy(d_cpow, cp.data(), cp.size() * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess)
+            return -EIO;
         for (uint32_t i = 0; i < n_downstreams; ++i) h_alive[i >> 6] |= 1ull << (i & 63);
         if (hipMemcpy(d_alive, h_alive, (nwords ? nwords : 1) * sizeof(uint64_t), hipMemcpyHostToDevice) !=
             hipSuccess)
@@ -148,6 +167,10 @@ struct DeviceState {
         (void)hipFree(d_alive);
         (void)hipFree(d_magic);
         (void)hipFree(d_kpow);
+        (void)hipFree(d_cpow);
+        (void)hipFree(d_tail);
+        d_cpow = nullptr;
+        d_tail = nullptr;
         (void)hipFree(d_ctl);
         (void)hipFree(d_status);
         (void)hipFree(d_bases);
@@ -191,6 +214,13 @@ struct DeviceState {
                 return -ENOMEM;
             }
         }
+        // two or more dead: the deferred probes keep hashes by record index; sized here for a batch
+        // of max_batch bytes (the router's one-batch launches), so that a data thread's launches never
+        // reallocate (hipFree / hipMalloc synchronise the device) in the middle of its stream
+        if (dead >= 2 && dead < nds) {
+            const int rc = reserve_defer(max_batch / SR_MIN_LINE_LENGTH + 1);
+            if (rc) return rc;
+        }
         if (dead && dead < nds && nds <= 64 * kAliveLds && !d_tile_pd &&
             hipMalloc(&d_tile_pd, (size_t)(max_tiles ? max_tiles : 1) * nwords * sizeof(uint64_t)) != hipSuccess) {
             d_tile_pd = nullptr;   // the launches replay the probes instead
@@ -227,6 +257,9 @@ struct DeviceState {
         p.tile_pd = d_tile_pd;
         p.dbg = nullptr;
         p.layout_out = d_layout;
+        p.cpow = d_cpow;
+        p.tail = d_tail;
+        p.lb_spin = lb_spin;
         return p;
     }
 
@@ -236,6 +269,10 @@ struct DeviceState {
     // first launch is one). Records are identical either way; only the time differs.
     bool choose_segments(hipStream_t stream) {
         bool seg;
+        if (layout_mode == SR_LAYOUT_CHUNKS) {
+            last_layout = SR_LAYOUT_CHUNKS;
+            return false;
+        }
         if (layout_mode == SR_LAYOUT_UNIFORM) {
             seg = false;
         } else if (layout_mode == SR_LAYOUT_SEGMENTS) {
@@ -387,7 +424,17 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
         }
     }
     if (ds.wide() && hipMemsetAsync(&ds.d_ctl->pending, 0, sizeof(uint32_t), stream) != hipSuccess) return -EIO;
-    hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
+    if constexpr ((ABL & KV_CHUNKS) != 0) {
+        static_assert(BLOCK == 256, "route_chunk_kernel: 256 lanes of 64 bytes per 16 KiB tile");
+        // its probe stops after the first picks: with two or more dead shards it needs the deferral
+        // (no scratch for it, e.g. inside a stream capture: the uniform kernel probes in full)
+        if (ds.dead >= 2 && ds.dead < ds.nds && !p.defer)
+            hipLaunchKernelGGL((route_kernel<BLOCK, KV_UNIFORM>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
+        else
+            hipLaunchKernelGGL((route_chunk_kernel<ABL>), dim3(p.total_blocks), dim3(256), 0, stream, p);
+    } else {
+        hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
+    }
     if (hipGetLastError() != hipSuccess) return -EIO;
     if (p.defer || p.mark) {   // the probes past their first two picks and the OR of the tiles' probed-dead
                                // slots (probe_defer_kernel), grid y = batch

@@ -188,6 +188,12 @@ struct RouteParams {
     uint64_t *dbg;           // ABL_STAMPS builds only: 16 timestamp slots per tile
     uint32_t *layout_out;    // host-mapped {sequence, tiles weighed, tiles segmented} of the last
                              // KV_SEGMENTS launch (null: not published)
+    // route_chunk_kernel (chunk_kernel.hpp): K^-z (z <= 64), then per lane K^(64 (255 - l)) and
+    // K^-(64 (255 - l)); per tile the tail-line granules {meta, hash lo, hash hi, -}; polls of a
+    // predecessor's tail granules before the tile computes that line itself (0: always)
+    const uint64_t *cpow;
+    uint64_t *tail;
+    uint32_t lb_spin;
     // per XCD class c, its batches in tile order: (class-local end tile << 6) | batch index;
     // ~0u after the last (one scalar load finds a tile's batch)
     uint32_t cls_tab[8][kPerClass];
@@ -938,11 +944,11 @@ __device__ __forceinline__ uint32_t stamp_block(const RouteParams &p, const Batc
     return p.xcd_local ? (bd.tile0 + t) * 8u + bd.cls : bd.tile0 + t;
 }
 
-template <int BLOCK, unsigned ABL>
-__device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint32_t epoch, SmemT<BLOCK> &sm,
+template <int BLOCK, unsigned ABL, class S>
+__device__ void scan_batch_split(const RouteParams &p, const BatchDesc &bd, uint32_t epoch, S &sm,
                                  int wave, int lane) {
     constexpr uint32_t kRing = 4096;
-    static_assert(SmemT<BLOCK>::kWords >= (int)kRing, "scanner ring in the LDS image");
+    static_assert(S::kWords >= (int)kRing, "scanner ring in the LDS image");
     uint32_t *const ring = sm.img;
     if (wave == 0) {
         constexpr int kGroups = 4;

@@ -75,7 +75,9 @@ static void free_ptr(void *p) { (void)hipFree(p); }
 // exist only in builds made with -DSR_ABLATION_VARIANTS (`make VARIANTS=1`, developer A/B runs;
 // never the shipped library): SR_VARIANT in the environment then selects one.
 static int launch_product(DeviceState &ds, const RouteParams &p, hipStream_t stream) {
-    if (ds.choose_segments(stream)) return launch_route<kBlock, KV_SEGMENTS>(ds, p, stream);
+    const bool seg = ds.choose_segments(stream);
+    if (ds.last_layout == SR_LAYOUT_CHUNKS) return launch_route<kBlock, KV_CHUNKS>(ds, p, stream);
+    if (seg) return launch_route<kBlock, KV_SEGMENTS>(ds, p, stream);
     return launch_route<kBlock, KV_UNIFORM>(ds, p, stream);
 }
 #ifdef SR_ABLATION_VARIANTS
@@ -211,7 +213,7 @@ int sr_set_stream(sr_ctx *c, void *stream) {
 }
 
 int sr_set_layout(sr_ctx *c, int layout) {
-    if (!c || layout < SR_LAYOUT_AUTO || layout > SR_LAYOUT_SEGMENTS) return -EINVAL;
+    if (!c || layout < SR_LAYOUT_AUTO || layout > SR_LAYOUT_CHUNKS) return -EINVAL;
     c->ds.layout_mode = layout;
     return 0;
 }

@@ -117,11 +117,13 @@ def test_generator_is_deterministic_and_framed(pkg, oracle):
 
 def test_product_library_has_only_the_product_route_kernels(pkg):
     """Ablation variants (some write wrong records by design) never ship: the product library holds
-    exactly the two lane layouts, KV_UNIFORM (0) and KV_SEGMENTS (4194304), which write identical
-    records (tests/test_gpu_layout.py); ablations live in tools/ and `make VARIANTS=1` builds only."""
+    exactly the three lane layouts, KV_UNIFORM (0), KV_SEGMENTS (4194304) and KV_CHUNKS (8388608,
+    route_chunk_kernel), which write identical records (tests/test_gpu_layout.py); ablations live in
+    tools/ and `make VARIANTS=1` builds only."""
     out = subprocess.run(["nm", "-C", pkg.ROUTE_LIB], capture_output=True, text=True).stdout
     kernels = {l.split(" ", 2)[-1] for l in out.splitlines()
-               if "route_kernel<" in l and "__device_stub__" not in l}
+               if ("route_kernel<" in l or "route_chunk_kernel<" in l) and "__device_stub__" not in l}
     assert kernels == {"void srk::route_kernel<256, 0u>(srk::RouteParams)",
-                       "void srk::route_kernel<256, 4194304u>(srk::RouteParams)"}, kernels
+                       "void srk::route_kernel<256, 4194304u>(srk::RouteParams)",
+                       "void srk::route_chunk_kernel<8388608u>(srk::RouteParams)"}, kernels
     assert b"SR_VARIANT" not in open(pkg.ROUTE_LIB, "rb").read()

@@ -1,7 +1,9 @@
-"""The route kernel's two lane layouts (sr_set_layout): KV_UNIFORM (one lane group per line, sized by
-the tile's mean line length) and KV_SEGMENTS (one lane per 64-byte name segment in tiles of mixed
-lengths) must give the same records and hashes bit for bit, both equal to the oracle; AUTO follows
-the segment statistics the kernel publishes. Needs an MI355X: `pytest -m gpu`."""
+"""The route kernel's lane layouts (sr_set_layout): KV_UNIFORM (one lane group per line, sized by
+the tile's mean line length), KV_SEGMENTS (one lane per 64-byte name segment in tiles of mixed
+lengths) and KV_CHUNKS (route_chunk_kernel: every lane hashes the 64 bytes it loaded, lines joined by
+a block scan and, across tiles, by the tail look-back) must give the same records and hashes bit for
+bit, all equal to the oracle; AUTO follows the segment statistics the kernel publishes. Needs an
+MI355X: `pytest -m gpu`."""
 from __future__ import annotations
 
 import hashlib
@@ -14,7 +16,8 @@ from test_gpu_parity import _assert_same, _hostile_stream, _lines_stream
 
 pytestmark = pytest.mark.gpu
 
-UNIFORM, SEGMENTS = 1, 2
+UNIFORM, SEGMENTS, CHUNKS = 1, 2, 3
+LAYOUTS = (UNIFORM, SEGMENTS, CHUNKS)
 
 
 def _streams(pkg):
@@ -34,7 +37,7 @@ def _streams(pkg):
 @pytest.mark.parametrize("n,dead", [(4, 0), (64, 0), (64, 20)])
 def test_layouts_match_oracle(pkg, oracle, n, dead):
     alive = [0 if i < dead else 1 for i in range(n)]
-    for layout in (UNIFORM, SEGMENTS):
+    for layout in LAYOUTS:
         r = pkg.Router(n, 4 << 20)
         try:
             r.set_alive(alive)
@@ -49,7 +52,7 @@ def test_layouts_match_oracle(pkg, oracle, n, dead):
 
 def test_layouts_full_size_digests(pkg):
     """The 16 MiB configuration digests (C2..C5) under each forced layout."""
-    for layout in (UNIFORM, SEGMENTS):
+    for layout in LAYOUTS:
         for key, d in sorted(load_digests().items()):
             s = pkg.gen_stream(d["nbytes"], d["line_lens"], seed=d["seed"], p_invalid=d["p_invalid"])
             words = np.array([int(x, 16) for x in d["alive"]], dtype=np.uint64)
@@ -92,7 +95,55 @@ def test_set_layout_rejects_unknown(pkg):
     r = pkg.Router(4, 1 << 20)
     try:
         with pytest.raises(pkg.SrError):
-            r.set_layout(3)
+            r.set_layout(4)
         assert r.last_layout() == 0
     finally:
         r.close()
+
+
+def _tile_straddles(rng):
+    """Lines placed so that 16 KiB tile boundaries fall before, on and after their first ':' and
+    their '\\n', plus lines longer than a tile (a tile with no '\\n' at all) and one-byte names."""
+    out = bytearray()
+    T = 16384
+    for k in range(40):
+        boundary = (len(out) // T + 1) * T
+        gap = boundary - len(out)
+        pre = int(rng.integers(0, 1500))
+        if gap > pre + 8:   # pad up to `pre` bytes before the boundary with short lines
+            fill = gap - pre
+            while fill > 0:
+                L = int(min(fill, rng.integers(6, 300)))
+                out += (b"p" * (L - 1) + b"\n") if L < 4 else (b"f" * (L - 4) + b":1|\n")[:L - 1] + b"\n"
+                fill -= L
+        kind = k % 5
+        L = int(rng.integers(8, 1449))
+        if kind == 4:
+            L = int(rng.integers(T + 10, 2 * T + 500))   # no '\n' in a whole tile
+        c = int(rng.integers(0, L - 1))
+        body = bytearray(rng.integers(97, 123, L - 1, dtype=np.uint8).tobytes())
+        if kind != 3:
+            body[c] = ord(":")
+        out += bytes(body) + b"\n"
+    out += b"x:1|c\n" * 10
+    return bytes(out)
+
+
+@pytest.mark.parametrize("spin", [None, "0"])
+def test_chunks_tile_straddles_and_lookback(pkg, oracle, monkeypatch, spin):
+    """KV_CHUNKS across tile boundaries: the straddling line from its predecessor's tail granules,
+    and (SR_LB_SPIN=0) from the global-memory fallback that runs when a predecessor never published."""
+    if spin is not None:
+        monkeypatch.setenv("SR_LB_SPIN", spin)
+    rng = np.random.default_rng(12)
+    for n, dead in [(4, 0), (64, 20), (7, 1)]:
+        alive = [0 if i < dead else 1 for i in range(n)]
+        r = pkg.Router(n, 4 << 20)
+        try:
+            r.set_alive(alive)
+            r.set_layout(CHUNKS)
+            for name, data in list(_streams(pkg)) + [("straddles", _tile_straddles(rng))]:
+                _assert_same(r.route(data, want_hashes=True), oracle.route(data, n, alive),
+                             f"{name} chunks N={n} dead={dead} spin={spin}")
+        finally:
+            r.close()

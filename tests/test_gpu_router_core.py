@@ -72,3 +72,60 @@ def test_core_metric_names_match_oracle(pkg):
             assert c.metric_name(i, 1) == t.traffic_name[i]
             assert c.metric_name(i, 2) == t.packet_name[i]
         assert c.metric_name(0, 3) == t.alive_metric
+
+
+@pytest.mark.parametrize("fail_at", [1, 3, 8])
+def test_core_async_submit_failure_loses_only_that_batch(pkg, monkeypatch, fail_at):
+    """A batch whose submission fails (fault injection: SR_CORE_FAIL_SUBMIT) is not taken: the caller
+    keeps filling the same slot, the batch in flight completes normally, and every later batch routes
+    from pending buffers the host and device agree on. The outcome equals the reference data thread
+    (oracle restatement) run on the session without that batch's datagrams."""
+    import sr_router_oracle as RO
+
+    monkeypatch.setenv("SR_CORE_FAIL_SUBMIT", str(fail_at))
+    core_mod = importlib.import_module("statsd-router_amd.core")
+    name = router_fixtures()[0]
+    f = load_router_fixture(name)
+    core = core_mod.Core(f["n"], f["ds_hosts"], f["ds_data_ports"], f["ping_prefix"], f["hostname"], f["data_port"],
+                         max_batch_bytes=1 << 20)
+    kept, pend, submits, failed = [], [], 0, 0
+
+    def flush_batch():
+        nonlocal submits, failed
+        if not pend:
+            return
+        submits += 1
+        try:
+            core.submit(pkg.frame_datagrams(pend))
+            kept.extend(("dgram", d) for d in pend)
+            assert core.in_flight() in (0, 1)
+        except pkg.SrError:
+            failed += 1
+            assert submits == fail_at
+            assert core.in_flight() != getattr(core, "_slot", 0)   # not taken: the slot stays free
+        pend.clear()
+
+    for e in f["events"]:
+        if e[0] == "dgram":
+            pend.append(e[1])
+            if len(pend) >= 7:
+                flush_batch()
+            continue
+        flush_batch()
+        kept.append(e)
+        if e[0] == "alive":
+            core.set_alive(e[1])
+        elif e[0] == "flush":
+            core.flush_timer()
+        elif e[0] == "ping":
+            core.ping()
+    flush_batch()
+    core.drain()
+    assert failed == 1 and core.in_flight() == -1
+    final = {s: core.state(s) for s in range(f["n"])}
+    core.close()
+    t = RO.DataThread(f["n"], f["ds_hosts"], f["ds_data_ports"], f["ping_prefix"], f["hostname"], f["data_port"])
+    t.run(kept)
+    assert core.logs == t.logs
+    assert {k: v for k, v in core.packets.items() if v} == {k: v for k, v in t.packets.items() if v}
+    assert final == t.final()

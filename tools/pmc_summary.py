@@ -25,8 +25,10 @@ def main():
         per = {}
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if "route_kernel" not in row["Kernel_Name"]:
+                kn = row["Kernel_Name"]
+                if "route_kernel" not in kn and "route_chunk_kernel" not in kn:
                     continue
+                meta.setdefault("kernel", "route_chunk_kernel" if "route_chunk_kernel" in kn else "route_kernel")
                 key = (row["Dispatch_Id"], row["Counter_Name"])
                 per[key] = per.get(key, 0.0) + float(row["Counter_Value"])
                 meta.setdefault("grid_size", int(row["Grid_Size"]))
@@ -37,7 +39,7 @@ def main():
         for (_, name), v in per.items():
             vals.setdefault(name, []).append(v)
     med = {k: statistics.median(v) for k, v in sorted(vals.items())}
-    res = {"config": config, "kernel": "route_kernel", "dispatches": max((len(v) for v in vals.values()), default=0),
+    res = {"config": config, "kernel": meta.get("kernel", "route_kernel"), "dispatches": max((len(v) for v in vals.values()), default=0),
            "median_per_dispatch": med, "kernel_meta": meta}
     if "FETCH_SIZE" in med:
         rd = 2.0 * med["FETCH_SIZE"] * 1024
