@@ -53,6 +53,10 @@ CONFIGS = {
            "c4_1024B_n16"),
     "c5": ("C5: 16 MiB batches of mixed 64/256/1024-byte metrics, 64 shards", 16 << 20, [64, 256, 1024], 0.0, 64,
            0x5EED0005, "c5_mixed_n64"),
+    # not a BASELINE configuration: statsd-sized lines whose ends fall anywhere in a 64-byte chunk
+    # (lane-layout A/B only; verified against the oracle, no reference digest)
+    "u1": ("U1: 16 MiB batches of 40/70/100/130-byte metrics, 16 shards", 16 << 20, [40, 70, 100, 130], 0.0, 16,
+           0x5EED0011, "u1_unaligned_n16"),
 }
 
 

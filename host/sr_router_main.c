@@ -164,8 +164,9 @@ static void udp_read_cb(struct ev_loop *loop, ev_io *w, int revents) {
     int batches = 0;
     for (;;) {
         if (d->cap - d->len < (size_t)RECV_VLEN * SR_DATA_BUF_SIZE) {
-            submit_batch(d);
-            if (++batches >= MAX_BATCHES_PER_READ) break;
+            if (d->c->dt_sync) route_batch(d);
+            else submit_batch(d);
+            if (d->c->dt_yield && ++batches >= d->c->dt_yield) break;
         }
         /* datagram j lands in its own 4096-byte slot after the batch's end, capped at 4095 bytes
          * like recv(fd, buffer, DATA_BUF_SIZE - 1) (sr-main.c:163), then is moved down and framed */
@@ -192,6 +193,10 @@ static void udp_read_cb(struct ev_loop *loop, ev_io *w, int revents) {
             d->len += n;
         }
         if (k < RECV_VLEN) break;   /* drained */
+    }
+    if (d->c->dt_sync) {
+        route_batch(d);
+        return;
     }
     submit_batch(d);
     ev_idle_start(d->loop, &d->idle);
@@ -338,6 +343,9 @@ int main(int argc, char *argv[]) {
     if (config.batch_bytes < (size_t)2 * RECV_VLEN * SR_DATA_BUF_SIZE) config.batch_bytes = (size_t)2 * RECV_VLEN * SR_DATA_BUF_SIZE;
     const char *nd = getenv("SR_DEVICES");
     config.n_devices = nd ? atoi(nd) : 1;
+    const char *ds = getenv("SR_DT_SYNC"), *dy = getenv("SR_DT_YIELD");
+    config.dt_sync = ds && ds[0] == '1';
+    config.dt_yield = dy ? atoi(dy) : MAX_BATCHES_PER_READ;
 
     struct ev_loop *loop = ev_default_loop(0);
     const char *fn = "main";

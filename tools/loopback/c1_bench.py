@@ -73,16 +73,24 @@ def main():
     ap.add_argument("--blasters", type=int, default=1, help="sender processes")
     ap.add_argument("--exe", action="append", default=[],
                     help="tag=path of another router executable to run the same way (A/B of builds)")
+    ap.add_argument("--var", action="append", default=[],
+                    help="tag:K=V,K=V - this build again with environment settings (A/B of data-thread modes)")
     a = ap.parse_args()
     import tempfile
 
     with tempfile.TemporaryDirectory() as tmp:
         exes = [("ours", OURS)] + ([("reference", REFERENCE)] if os.path.exists(REFERENCE) else [])
-        exes += [tuple(e.split("=", 1)) for e in a.exe]
-        for tag, exe in exes:
-            if a.only and tag != a.only and tag not in {e.split("=", 1)[0] for e in a.exe}:
+        exes = [(t, e, None) for t, e in exes] + [tuple(e.split("=", 1)) + (None,) for e in a.exe]
+        for v in a.var:
+            tag, kv = v.split(":", 1)
+            env = dict(os.environ, **dict(x.split("=", 1) for x in kv.split(",") if x))
+            exes.append((tag, OURS, env))
+        extra = {e[0] for e in exes[2:]}
+        for tag, exe, env in exes:
+            if a.only and tag != a.only and tag not in extra:
                 continue
-            print(json.dumps(dict(run(exe, a.seconds, a.threads, a.rate, a.dgram, tmp, nblast=a.blasters), kind=tag)), flush=True)
+            print(json.dumps(dict(run(exe, a.seconds, a.threads, a.rate, a.dgram, tmp, env=env, nblast=a.blasters),
+                                  kind=tag)), flush=True)
 
 
 if __name__ == "__main__":
