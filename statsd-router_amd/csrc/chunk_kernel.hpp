@@ -32,6 +32,9 @@
 namespace srk {
 
 constexpr unsigned KV_CHUNKS = 8388608u;       // the chunk-layout kernel (route_chunk_kernel)
+// developer ablations of route_chunk_kernel (timing / counter attribution only, wrong records; built
+// with -DSR_CHUNK_ABL=<mask> into tools/ab, never shipped)
+enum : unsigned { CH_ABL_NO_U = 1u << 24, CH_ABL_NO_SUF = 1u << 25, CH_ABL_NO_EMIT = 1u << 26 };
 constexpr int kCinv = 65;                      // K^-z, z = 0 .. 64
 constexpr int kCpowEntries = kCinv + 2 * 256;  // + K^(64 (255 - l)), K^-(64 (255 - l)) per lane l
 constexpr uint32_t kFlagTail = 1u;             // tail granules (flag field of mk_status)
@@ -72,6 +75,14 @@ __device__ __forceinline__ uint64_t row_horner(const uint32_t *row, const uint64
     if (m < F) h = sdbm_dword_fast(h, q[m++]);
     if (rem) h = h * kp_lo[rem] + sdbm_dword_fast(0, q[m] << (8 * (4 - rem)));
     return h;
+}
+
+// 16 bytes at `a` by byte loads: bytes past the buffer's range read as 0, exactly
+__device__ __forceinline__ uint4 load16_bytes(__amdgpu_buffer_rsrc_t rsrc, uint32_t a) {
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) w[i >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, a + i, 0, 0) << (8 * (i & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
 // Wave-cooperative helpers of the look-back fallback (a predecessor that never published, or a
@@ -138,8 +149,8 @@ __device__ __forceinline__ void pin64(uint64_t &x) {
 // pads, the dead shards visited noted in the tile's LDS words (MARK_LDS).
 __device__ __forceinline__ uint32_t chunk_probe(uint64_t h, const RouteParams &p, uint32_t *img) {
     const uint32_t n = p.nds;
+    if (p.dead >= n) return SR_ROUTE_ALL_DEAD;   // includes N == 0 (:115-116)
     if (p.dead == 0) return mod_magic(h, p.magic_n, n);
-    if (p.dead >= n) return SR_ROUTE_ALL_DEAD;
     const bool small = n <= 64;
     const uint64_t alive0 = small ? ((uint64_t)alive_pad_dword(img, 32) << 32) | alive_pad_dword(img, 0) : 0ull;
     const int np = p.dead >= 2 && p.picks == 1 ? 1 : 2;
@@ -208,18 +219,14 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     constexpr int kKpWords = 2 * (kPowLo + kPowHi);
     const uint32_t kw = ((const uint32_t *)p.kpow)[tid < kKpWords ? tid : kKpWords - 1];
     const uint32_t iw = ((const uint32_t *)p.cpow)[tid < 2 * kCinv ? tid : 2 * kCinv - 1];
-    if (T0 + 16384u > nbytes) {   // the batch's last tile: bytes past its end read as 0
+    if (T0 + 16384u > nbytes) {
+        // the batch's last tile: a piece past the end reads as zeros, but the range check of a 16-byte
+        // load that straddles the end is not byte-exact (its bytes before the end can read as zero
+        // too): that one piece is read again byte by byte (byte loads are range-checked exactly)
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int r = (int)(nbytes - T0) - (o + 16 * k);   // bytes of this piece in the batch
-            auto keep = [&](int d) {
-                const int n = min(max(r - 4 * d, 0), 4);
-                return n >= 4 ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
-            };
-            v[k].x &= keep(0);
-            v[k].y &= keep(1);
-            v[k].z &= keep(2);
-            v[k].w &= keep(3);
+            const uint32_t a = T0 + (uint32_t)o + 16u * k;
+            if (a < nbytes && a + 16u > nbytes) v[k] = load16_bytes(rsrc, a);
         }
     }
     const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -235,8 +242,8 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         sm.img[(uint32_t)tid * 17 + 16] = 0u;
     if (tid == 0) sm.hs[kSlotBefore] = 0ull;
 
-    // ---- the chunk: LDS row, '\n' / ':' masks, U -----------------------------------------------
-    uint64_t nlm, clm, U;
+    // ---- the chunk: LDS row, '\n' / ':' masks ------------------------------------------------
+    uint64_t nlm, clm;
     {
         const uint32_t rb = lds_addr(&sm.img[tid * 17]);
         ds_write2_at<0, 1>(rb, v[0].x, v[0].y);
@@ -247,6 +254,7 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         ds_write2_at<10, 11>(rb, v[2].z, v[2].w);
         ds_write2_at<12, 13>(rb, v[3].x, v[3].y);
         ds_write2_at<14, 15>(rb, v[3].z, v[3].w);
+        stamp<ABL>(p, tid, g, 0);   // (the row's stores need the loads: they have arrived)
         uint32_t m[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) m[k] = nl_colon_mask16(v[k]);
@@ -254,15 +262,6 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         clm = ((uint64_t)__builtin_amdgcn_perm(m[3], m[2], 0x07060302u) << 32) | __builtin_amdgcn_perm(m[1], m[0], 0x07060302u);
         pin64(nlm);
         pin64(clm);
-        U = sdbm_qword_fast(0ull, v[0].x, v[0].y);
-        U = sdbm_qword_fast(U, v[0].z, v[0].w);
-        U = sdbm_qword_fast(U, v[1].x, v[1].y);
-        U = sdbm_qword_fast(U, v[1].z, v[1].w);
-        U = sdbm_qword_fast(U, v[2].x, v[2].y);
-        U = sdbm_qword_fast(U, v[2].z, v[2].w);
-        U = sdbm_qword_fast(U, v[3].x, v[3].y);
-        U = sdbm_qword_fast(U, v[3].z, v[3].w);
-        pin64(U);   // materialised here: sunk to its late uses it would keep 32 pair products live
     }
     if (tid < kKpWords) ((uint32_t *)&sm.kp_lo[0])[tid] = kw;   // kp_lo | kp_hi are contiguous
     if (tid < 2 * kCinv) ((uint32_t *)&sm.kinv[0])[tid] = iw;
@@ -320,9 +319,24 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     const bool before = prevnl == 0 && !sm.head_nl;                      // ... which began in an earlier tile
     const uint32_t ih = before ? kSlotBefore : (uint32_t)prevnl >> 6;   // its slot
 
+    // ---- U: Horner of the chunk's 64 bytes, from its LDS row. After the count is published: a
+    // tile's record base follows its predecessors' counts through the scanner, so the earlier the
+    // counts go out, the less the tiles wait for their bases when they write their records ----------
+    const uint32_t *const row = &sm.img[tid * 17];
+    uint64_t U;
+    {
+        uint32_t x[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = row[i];
+        U = sdbm_qword_fast(0ull, x[0], x[1]);
+#pragma unroll
+        for (int i = 2; i < 16; i += 2) U = sdbm_qword_fast(U, x[i], x[i + 1]);
+        if (ABL & CH_ABL_NO_U) U = x[0];
+        pin64(U);   // materialised here: sunk to its late uses it would keep 32 pair products live
+    }
+
     // ---- the positions that need H: the open line's first ':' in this chunk, the chunk's tail line
     // (after its last '\n') and that line's first ':' ----------------------------------------------
-    const uint32_t *const row = &sm.img[tid * 17];
     const int firstnl = nlm ? __builtin_ctzll(nlm) : 64;
     const uint64_t c0m = clm & (firstnl == 64 ? ~0ull : ((1ull << firstnl) - 1ull));
     const bool ev1 = ofc == kNone && c0m != 0ull;                         // the open line's first ':'
@@ -334,10 +348,10 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         return back ? r : U - r * sm.kp_lo[(64 - q) & 63];
     };
     uint64_t S1 = 0, S2 = 0, S3 = 0;
-    if (__ballot(ev1)) {
+    if (!(ABL & CH_ABL_NO_SUF) && __ballot(ev1)) {
         if (ev1) S1 = suf(__builtin_ctzll(c0m));
     }
-    if (__ballot(has_tail)) {
+    if (!(ABL & CH_ABL_NO_SUF) && __ballot(has_tail)) {
         if (has_tail) S2 = suf(lastnl + 1);
         if (ev3) S3 = suf(__builtin_ctzll(cafter));
     }
@@ -396,7 +410,13 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     {
         const uint64_t st = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(bst >> 32)) << 32) |
                             (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)bst);
-        base = granule_ok(st, ep0 & 0x3FFFFFFFu, kFlagBase) ? (uint32_t)st : wait_base(base_slot, ep0, rsrc, T0);
+        if (granule_ok(st, ep0 & 0x3FFFFFFFu, kFlagBase)) {
+            base = (uint32_t)st;
+        } else {
+            stamp<ABL>(p, tid, g, 3);
+            base = wait_base(base_slot, ep0, rsrc, T0);
+            stamp<ABL>(p, tid, g, 7);
+        }
         base = __builtin_amdgcn_readfirstlane(base);
     }
     auto emit = [&](int j, uint32_t off, int len, bool len_ok, bool fmt_ok, uint64_t h) {
@@ -434,7 +454,7 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     }
     // every line that ends in the chunk, in order (the first one later if it began in an earlier
     // tile); the further lines of a chunk with several '\n' (lines under 64 bytes) lie within it
-    {
+    if (!(ABL & CH_ABL_NO_EMIT)) {
         uint64_t rest = nlm;
         int prev = -1, j = lf;
         while (rest) {
@@ -473,10 +493,11 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     }
     stamp<ABL>(p, tid, g, 5);
 
+    stamp<ABL>(p, tid, g, 6);
     // ---- the line that began in an earlier tile: its predecessor's tail granules ----------------
     const bool lb = nlm != 0ull && before;
     const uint64_t lbm = __ballot(lb);
-    if (lbm) {
+    if (!(ABL & CH_ABL_NO_EMIT) && lbm) {
         const int L = __builtin_ctzll(lbm);
         const uint64_t *const tg = p.tail + (size_t)(bd.sbase + t - 1u) * 4u;
         const uint32_t ep = ep0 & 0x3FFFFFFFu;

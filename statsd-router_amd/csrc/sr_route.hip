@@ -70,13 +70,17 @@ struct sr_ctx {
 
 static void free_ptr(void *p) { (void)hipFree(p); }
 
+#ifndef SR_CHUNK_ABL
+#define SR_CHUNK_ABL 0u   // developer ablation builds of route_chunk_kernel only (chunk_kernel.hpp)
+#endif
+
 // The product launches KV_UNIFORM or KV_SEGMENTS (identical records; DeviceState::choose_segments
 // picks by the lane-layout policy). Ablation variants (records wrong by design in some of them)
 // exist only in builds made with -DSR_ABLATION_VARIANTS (`make VARIANTS=1`, developer A/B runs;
 // never the shipped library): SR_VARIANT in the environment then selects one.
 static int launch_product(DeviceState &ds, const RouteParams &p, hipStream_t stream) {
     const bool seg = ds.choose_segments(stream);
-    if (ds.last_layout == SR_LAYOUT_CHUNKS) return launch_route<kBlock, KV_CHUNKS>(ds, p, stream);
+    if (ds.last_layout == SR_LAYOUT_CHUNKS) return launch_route<kBlock, KV_CHUNKS | SR_CHUNK_ABL>(ds, p, stream);
     if (seg) return launch_route<kBlock, KV_SEGMENTS>(ds, p, stream);
     return launch_route<kBlock, KV_UNIFORM>(ds, p, stream);
 }

@@ -32,7 +32,7 @@ static double med(std::vector<double> v) {
 
 // one launch over all L batches (the product's multi-batch mode): per-phase medians over every
 // workgroup of the launch, plus the launch span
-static bool seg_layout = false;
+static bool seg_layout = false, chunk_layout = false;
 
 template <int BLOCK>
 void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size_t> &sizes, sr_record *d_out,
@@ -47,7 +47,8 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
         for (int i = 0; i < L; ++i)
             DeviceState::add_batch(p, batches[i], sizes[i], d_out + (size_t)i * max_lines, max_lines, nullptr, d_n + i);
         p.dbg = d_dbg;
-        if (seg_layout) launch_route<BLOCK, ABL_STAMPS | KV_SEGMENTS>(ds, p, s);
+        if (chunk_layout) launch_route<BLOCK, ABL_STAMPS | KV_CHUNKS>(ds, p, s);
+        else if (seg_layout) launch_route<BLOCK, ABL_STAMPS | KV_SEGMENTS>(ds, p, s);
         else launch_route<BLOCK, ABL_STAMPS>(ds, p, s);
     };
     for (int w = 0; w < 3; ++w) launch();
@@ -174,10 +175,13 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
 int main(int argc, char **argv) {
     const int L = 16;
     const size_t batch = 16u << 20;
-    // argv: line length (0 = the C5 mix 64/256/1024), shards, "seg" for the segment layout
+    // argv: line length (0 = the C5 mix 64/256/1024), shards, "seg" / "chunks" for those layouts
     uint32_t line_len = argc > 1 ? (uint32_t)atoi(argv[1]) : 64;
     const uint32_t nds = argc > 2 ? (uint32_t)atoi(argv[2]) : 4;
     seg_layout = argc > 3 && !strcmp(argv[3], "seg");
+    chunk_layout = argc > 3 && !strcmp(argv[3], "chunks");   // route_chunk_kernel: stamps 0 loads in, 1 after
+                                                             // the count barrier, 2 Suf done, 4 slots done,
+                                                             // 5 records, 6 before the look-back, 9 exit
     uint32_t mix[3] = {64, 256, 1024};
     const uint32_t *lens = line_len ? &line_len : mix;
     const uint32_t nlens = line_len ? 1u : 3u;
