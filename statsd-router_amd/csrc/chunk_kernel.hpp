@@ -296,7 +296,6 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         granule_store(&p.status[bd.sbase + t], mk_status(ep0, kFlagAgg, tile_count | ((8u | x) << 28)), same);
     }
     const uint64_t *const base_slot = p.bases + bd.sbase + t;
-    const uint64_t bst = __hip_atomic_load(base_slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // used late
     const bool long_tile = (tflags & 2u) != 0;
     // the lane's exclusive state: lines before its chunk, the last '\n' before it (+ 1), and the
     // first ':' of the line open at its start (route_kernel's lane_state)
@@ -406,17 +405,40 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     stamp<ABL>(p, tid, g, 4);
 
     // ---- records ------------------------------------------------------------------------------
-    uint32_t base;
-    {
-        const uint64_t st = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(bst >> 32)) << 32) |
-                            (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)bst);
-        if (granule_ok(st, ep0 & 0x3FFFFFFFu, kFlagBase)) {
-            base = (uint32_t)st;
-        } else {
-            stamp<ABL>(p, tid, g, 3);
-            base = wait_base(base_slot, ep0, rsrc, T0);
-            stamp<ABL>(p, tid, g, 7);
+    // The tile's first record index: the freshest base the scanner has published among the 64 tiles
+    // up to this one, plus the counts published since (each wave on its own, one round trip per try).
+    // The scanner needs ~1.2 us to turn a count into a base; a chunk-layout tile publishes its count
+    // only ~1.3 us before it writes its records, so waiting for the scanner's base of this very tile
+    // cost 1.7 us per tile (stamps).
+    uint32_t base = 0;
+    if (t > 0) {
+        const uint32_t ep = ep0 & 0x3FFFFFFFu;
+        const int c = (int)t - lane;       // lane l: the scanner's base of tile t - l ...
+        const int cc = c - 1;              // ... and the count of tile t - 1 - l
+        bool done = false;
+        for (uint32_t spin = 0; spin < (uint32_t)kSpinBudget && !done; ++spin) {
+            const uint64_t bg = __hip_atomic_load(&p.bases[bd.sbase + (uint32_t)max(c, 0)], __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t cg = __hip_atomic_load(&p.status[bd.sbase + (uint32_t)max(cc, 0)], __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+            const bool bok = c == 0 || (c > 0 && granule_ok(bg, ep, kFlagBase));   // tile 0's base is 0
+            const bool cok = cc >= 0 && granule_ok(cg, ep, kFlagAgg);
+            const uint64_t okc = __ballot(cok);
+            const int nc = ~okc ? __builtin_ctzll(~okc) : 64;   // counts of tiles t-1 .. t-nc are in
+            const uint64_t cand = __ballot(bok && lane <= nc);
+            if (cand) {
+                const int l = __builtin_ctzll(cand);
+                const uint32_t pre = wave_incl_add32(cok ? ((uint32_t)cg & kCountMask) : 0u);
+                base = (uint32_t)__builtin_amdgcn_readlane((int)(c > 0 ? (uint32_t)bg : 0u), l) +
+                       (l ? (uint32_t)__builtin_amdgcn_readlane((int)pre, l - 1) : 0u);
+                done = true;
+            } else {
+                if (spin == 0) stamp<ABL>(p, tid, g, 3);
+                __builtin_amdgcn_s_sleep(1);
+            }
         }
+        if (!done) base = wait_base(base_slot, ep0, rsrc, T0);
+        stamp<ABL>(p, tid, g, 7);
         base = __builtin_amdgcn_readfirstlane(base);
     }
     auto emit = [&](int j, uint32_t off, int len, bool len_ok, bool fmt_ok, uint64_t h) {
@@ -443,52 +465,47 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     };
     // The chunk's first line: its name hash within the tile, h = K^(c' - 64) (H(c) - K^(64 (lc - ls)) H(s))
     // (H(s) = 0 for a line that began in an earlier tile: its earlier part comes from the look-back).
+    // A line within the chunk (C2: every line) is K^(c' - 64) (U - Suf(c')): no slots, no Y.
     const int c_first = ofc != kNone ? ofc : (c0m ? o + __builtin_ctzll(c0m) : kNone);
     const int e0 = o + firstnl;
     uint64_t hin0 = 0;
     if (nlm && c_first != kNone && c_first < e0) {
-        const uint64_t hcv = c_first >= o ? Y - S1 : sm.hc[ih];
-        const uint64_t hsv = before ? 0ull : (prevnl == o ? Y - U : sm.hs[ih]);
-        const int d = before ? 0 : min((c_first >> 6) - (prevnl >> 6), kPowHi - 1);   // <= 23 for valid lines
-        hin0 = sm.kinv[64 - (c_first & 63)] * (hcv - sm.kp_hi[d] * hsv);
+        if (prevnl == o && !before) {
+            hin0 = sm.kinv[64 - (c_first & 63)] * (U - S1);
+        } else {
+            const uint64_t hcv = c_first >= o ? Y - S1 : sm.hc[ih];
+            const uint64_t hsv = before ? 0ull : sm.hs[ih];
+            const int d = before ? 0 : min((c_first >> 6) - (prevnl >> 6), kPowHi - 1);   // <= 23 for valid lines
+            hin0 = sm.kinv[64 - (c_first & 63)] * (hcv - sm.kp_hi[d] * hsv);
+        }
     }
-    // every line that ends in the chunk, in order (the first one later if it began in an earlier
-    // tile); the further lines of a chunk with several '\n' (lines under 64 bytes) lie within it
     if (!(ABL & CH_ABL_NO_EMIT)) {
-        uint64_t rest = nlm;
-        int prev = -1, j = lf;
-        while (rest) {
-            const int eb = __builtin_ctzll(rest);
-            rest &= rest - 1ull;
-            int len;
-            uint32_t off;
-            bool fmt_ok;
-            uint64_t h = 0;
-            if (prev < 0) {
-                if (before) {   // finished below, from the earlier tile's tail granules
-                    prev = eb;
-                    ++j;
-                    continue;
-                }
-                off = T0 + (uint32_t)prevnl;
-                len = e0 - prevnl + 1;
-                fmt_ok = c_first != kNone && c_first < e0;   // :140
-                h = hin0;
-            } else {
-                off = T0 + (uint32_t)(o + prev + 1);
-                len = eb - prev;
+        if (nlm && !before) {   // the chunk's first line (one that began in an earlier tile: below)
+            const int len = e0 - prevnl + 1;
+            const bool len_ok = len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH;   // :180
+            const bool fmt_ok = c_first != kNone && c_first < e0;                                  // :140
+            emit(lf, T0 + (uint32_t)prevnl, len, len_ok, fmt_ok, len_ok && fmt_ok ? hin0 : 0ull);
+        }
+        // further lines of a chunk with several '\n' (lines under 64 bytes): within the chunk
+        if (__ballot(__popcll(nlm) > 1)) {
+            uint64_t rest = nlm & (nlm - 1ull);
+            int prev = firstnl, j = lf + 1;
+            while (rest) {
+                const int eb = __builtin_ctzll(rest);
+                rest &= rest - 1ull;
+                const int len = eb - prev;
                 const uint64_t cm = clm & ((1ull << eb) - 1ull) & (~0ull << (prev + 1));
-                fmt_ok = cm != 0ull;
-                if (fmt_ok) {
+                const bool len_ok = len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH;
+                const bool fmt_ok = cm != 0ull;
+                uint64_t h = 0;
+                if (len_ok && fmt_ok) {
                     const int cq = __builtin_ctzll(cm);
                     h = sm.kinv[64 - cq] * (suf(prev + 1) - suf(cq));
                 }
+                emit(j, T0 + (uint32_t)(o + prev + 1), len, len_ok, fmt_ok, h);
+                prev = eb;
+                ++j;
             }
-            const bool len_ok = len >= (int)SR_MIN_LINE_LENGTH && len <= (int)SR_MAX_LINE_LENGTH;   // :180
-            if (!(len_ok && fmt_ok)) h = 0;
-            emit(j, off, len, len_ok, fmt_ok, h);
-            prev = eb;
-            ++j;
         }
     }
     stamp<ABL>(p, tid, g, 5);
