@@ -57,6 +57,7 @@ typedef struct sr_config {
     int dt_sync;                                /* SR_DT_SYNC=1: every read event routes and completes its */
                                                 /* batch before returning (no double buffering; A/B)    */
     int dt_yield;                               /* full batches per read event before timers run (0: no cap) */
+    double dt_yield_s;                          /* seconds per read event before timers run (0: no cap)  */
     /* alive bits published by the health checker to the data threads */
     _Atomic uint64_t alive_gen;
     _Atomic uint64_t *alive_words;

@@ -28,7 +28,7 @@
 
 #define RECV_VLEN 256      /* datagrams per recvmmsg call */
 #define SEND_VLEN 512      /* packets per sendmmsg call */
-#define MAX_BATCHES_PER_READ 4   /* full batches per read event before the loop runs its timers again */
+#define READ_EVENT_SECONDS 0.02  /* a read event returns to the loop (its timers) after this long */
 
 typedef struct data_thread {
     sr_thread *t;
@@ -158,15 +158,19 @@ static void udp_read_cb(struct ev_loop *loop, ev_io *w, int revents) {
         sr_log(SR_WARN, "%s: invalid event %s", "udp_read_cb", strerror(errno));
         return;
     }
-    /* Under sustained load the socket never drains: after MAX_BATCHES_PER_READ full batches the event
-     * returns to the loop (the socket is still readable, so it comes straight back), and the flush,
-     * ping and alive updates run in between, as they do between the reference's one-datagram reads. */
+    /* Under sustained load the socket never drains: after READ_EVENT_SECONDS (checked at each full
+     * batch) the event returns to the loop (the socket is still readable, so it comes straight back),
+     * and the flush, ping and alive timers run in between, as they do between the reference's
+     * one-datagram reads. A cap of 4 batches per event instead cost a third of the delivered lines at
+     * one data thread and two senders (profiles/r04/c1_ab_r4g.jsonl). */
     int batches = 0;
+    const ev_tstamp t0 = d->c->dt_yield_s > 0 ? ev_time() : 0;
     for (;;) {
         if (d->cap - d->len < (size_t)RECV_VLEN * SR_DATA_BUF_SIZE) {
             if (d->c->dt_sync) route_batch(d);
             else submit_batch(d);
             if (d->c->dt_yield && ++batches >= d->c->dt_yield) break;
+            if (d->c->dt_yield_s > 0 && ev_time() - t0 >= d->c->dt_yield_s) break;
         }
         /* datagram j lands in its own 4096-byte slot after the batch's end, capped at 4095 bytes
          * like recv(fd, buffer, DATA_BUF_SIZE - 1) (sr-main.c:163), then is moved down and framed */
@@ -343,9 +347,10 @@ int main(int argc, char *argv[]) {
     if (config.batch_bytes < (size_t)2 * RECV_VLEN * SR_DATA_BUF_SIZE) config.batch_bytes = (size_t)2 * RECV_VLEN * SR_DATA_BUF_SIZE;
     const char *nd = getenv("SR_DEVICES");
     config.n_devices = nd ? atoi(nd) : 1;
-    const char *ds = getenv("SR_DT_SYNC"), *dy = getenv("SR_DT_YIELD");
+    const char *ds = getenv("SR_DT_SYNC"), *dy = getenv("SR_DT_YIELD"), *dys = getenv("SR_DT_YIELD_S");
     config.dt_sync = ds && ds[0] == '1';
-    config.dt_yield = dy ? atoi(dy) : MAX_BATCHES_PER_READ;
+    config.dt_yield = dy ? atoi(dy) : 0;
+    config.dt_yield_s = dys ? atof(dys) : READ_EVENT_SECONDS;
 
     struct ev_loop *loop = ev_default_loop(0);
     const char *fn = "main";

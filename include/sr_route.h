@@ -98,10 +98,14 @@ int sr_set_stream(sr_ctx *ctx, void *stream);
  *                      line length (best for uniform lengths);
  *   SR_LAYOUT_SEGMENTS a tile of mixed lengths gets one lane per 64-byte name segment, lines packed
  *                      back to back (best when short and long lines share tiles);
- *   SR_LAYOUT_AUTO     (default) segments while at least a quarter of the tiles of the last
- *                      segment-layout launch took it (back below a tenth); uniform otherwise, with
- *                      every 32nd launch outside stream capture (and the first) a segment-layout
- *                      probe. A graph captured from the context keeps the layout of its capture.
+ *   SR_LAYOUT_CHUNKS   every lane hashes the 64 bytes it loaded; lines spanning lanes are joined
+ *                      by a block scan of partial hashes, lines spanning tiles by a look-back
+ *                      (independent of the line lengths; best for mixed lengths);
+ *   SR_LAYOUT_AUTO     (default) every 32nd launch outside stream capture (and the first) is a
+ *                      segment-layout probe that weighs the traffic; chunks while at least a quarter
+ *                      of the tiles of the last probe took the segment layout (back below a tenth),
+ *                      uniform otherwise. A graph captured from the context keeps the layout of its
+ *                      capture.
  * Returns 0 or -EINVAL. */
 #define SR_LAYOUT_AUTO 0
 #define SR_LAYOUT_UNIFORM 1
@@ -109,7 +113,7 @@ int sr_set_stream(sr_ctx *ctx, void *stream);
 #define SR_LAYOUT_CHUNKS 3
 int sr_set_layout(sr_ctx *ctx, int layout);
 
-/* The layout the last route launch of the context used (SR_LAYOUT_UNIFORM or SR_LAYOUT_SEGMENTS;
+/* The layout the last route launch of the context used (SR_LAYOUT_UNIFORM, _SEGMENTS or _CHUNKS;
  * 0 before the first launch), or -EINVAL. */
 int sr_last_layout(const sr_ctx *ctx);
 

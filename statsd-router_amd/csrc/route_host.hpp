@@ -263,10 +263,10 @@ struct DeviceState {
         return p;
     }
 
-    // The route kernel variant for the next launch. AUTO: switch to KV_SEGMENTS when at least a
-    // quarter of the tiles a KV_SEGMENTS launch weighed took the segment layout, back below a
-    // tenth; while uniform, every 32nd launch outside stream capture is a KV_SEGMENTS probe (the
-    // first launch is one). Records are identical either way; only the time differs.
+    // The route kernel variant for the next launch. AUTO: switch to the chunk layout when at least
+    // a quarter of the tiles a KV_SEGMENTS launch weighed took the segment layout, back below a
+    // tenth; every 32nd launch outside stream capture is a KV_SEGMENTS probe that weighs the
+    // traffic (the first launch is one). Records are identical either way; only the time differs.
     bool choose_segments(hipStream_t stream) {
         bool seg;
         if (layout_mode == SR_LAYOUT_CHUNKS) {
@@ -288,8 +288,14 @@ struct DeviceState {
             }
             hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
             const bool capturing = hipStreamIsCapturing(stream, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
-            seg = seg_on || (!capturing && launches % 32 == 0);
+            const bool probe = !capturing && launches % 32 == 0;
             if (!capturing) ++launches;
+            // mixed traffic goes to the chunk layout; the probes keep weighing it with KV_SEGMENTS
+            if (seg_on && !probe) {
+                last_layout = SR_LAYOUT_CHUNKS;
+                return false;
+            }
+            seg = probe;
         }
         last_layout = seg ? SR_LAYOUT_SEGMENTS : SR_LAYOUT_UNIFORM;
         return seg;

@@ -69,8 +69,9 @@ def test_layouts_full_size_digests(pkg):
 
 
 def test_auto_follows_the_traffic(pkg, oracle):
-    """AUTO: the first launch probes the segment layout; mixed-length traffic keeps it, uniform
-    traffic drops back to the uniform layout until the next probe (every 32nd launch)."""
+    """AUTO: the first launch probes the traffic with the segment layout; mixed-length traffic
+    switches to the chunk layout, uniform traffic drops back to the uniform layout; every 32nd
+    launch probes again."""
     mixed = pkg.gen_stream(4 << 20, [64, 256, 1024], seed=0x5EED0005).data
     uniform = pkg.gen_stream(4 << 20, [1024], seed=0x5EED0004).data
     r = pkg.Router(64, 4 << 20)
@@ -79,14 +80,17 @@ def test_auto_follows_the_traffic(pkg, oracle):
         for data in [mixed, mixed, mixed, uniform, uniform, uniform]:
             _assert_same(r.route(data, want_hashes=True), oracle.route(data, 64), "auto")
             seen.append(r.last_layout())
-        assert seen[:3] == [SEGMENTS] * 3
-        assert seen[3] == SEGMENTS            # decided before the uniform batch's statistics
-        assert seen[4:] == [UNIFORM, UNIFORM]
-        for _ in range(32 - len(seen)):       # launches 6..31 stay uniform
+        assert seen == [SEGMENTS] + [CHUNKS] * 5   # chunk launches publish no statistics
+        for _ in range(32 - len(seen)):       # launches 6..31 stay on the chunk layout
+            r.route(uniform)
+            assert r.last_layout() == CHUNKS
+        _assert_same(r.route(uniform, want_hashes=True), oracle.route(uniform, 64), "probe")
+        assert r.last_layout() == SEGMENTS    # launch 32: a probe, weighing uniform traffic
+        for _ in range(3):
             r.route(uniform)
             assert r.last_layout() == UNIFORM
-        r.route(uniform)                      # launch 32: a probe
-        assert r.last_layout() == SEGMENTS
+        r.route(mixed)                        # decided before this batch's statistics
+        assert r.last_layout() == UNIFORM
     finally:
         r.close()
 

@@ -59,6 +59,10 @@ def run(exe, seconds, threads, rate, dgram, tmp, env=None, nblast=1):
         # datagrams past the blast; the sink's span also covers the last flush-timer tick)
         "delivered_lines_per_blast_s": round(got["lines"] / sent["seconds"], 1),
         "delivered_fraction": round(got["lines"] / max(sent["lines"], 1), 4),
+        # the sink's first / last datagram against the first sender's start and the last sender's end
+        # (one CLOCK_MONOTONIC): the span's head and the tail after the blast (flush-timer ticks)
+        "sink_head_s": round(got["first_abs"] - min(o["start_abs"] for o in outs), 4) if "first_abs" in got else None,
+        "sink_tail_s": round(got["last_abs"] - max(o["end_abs"] for o in outs), 4) if "last_abs" in got else None,
         "downstream_packets": got["datagrams"],
     }
 

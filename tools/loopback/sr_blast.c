@@ -123,7 +123,8 @@ int main(int argc, char **argv) {
         dg += (uint64_t)r;
         pi = (pi + r) % POOL;
     }
-    printf("{\"datagrams\": %llu, \"lines\": %llu, \"bytes\": %llu, \"seconds\": %.6f}\n", (unsigned long long)dg,
-           (unsigned long long)lines, (unsigned long long)bytes, t - t0);
+    printf("{\"datagrams\": %llu, \"lines\": %llu, \"bytes\": %llu, \"seconds\": %.6f, \"start_abs\": %.6f, "
+           "\"end_abs\": %.6f}\n",
+           (unsigned long long)dg, (unsigned long long)lines, (unsigned long long)bytes, t - t0, t0, t);
     return 0;
 }

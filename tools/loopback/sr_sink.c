@@ -153,8 +153,9 @@ int main(int argc, char **argv) {
                (unsigned long long)lines[i], (unsigned long long)bytes[i]);
         td += dg[i], tl += lines[i], tb += bytes[i];
     }
-    printf("], \"datagrams\": %llu, \"lines\": %llu, \"bytes\": %llu, \"first\": %.6f, \"last\": %.6f}\n",
+    printf("], \"datagrams\": %llu, \"lines\": %llu, \"bytes\": %llu, \"first\": %.6f, \"last\": %.6f, "
+           "\"first_abs\": %.6f, \"last_abs\": %.6f}\n",
            (unsigned long long)td, (unsigned long long)tl, (unsigned long long)tb, first > 0 ? first - t0 : -1.0,
-           last > 0 ? last - t0 : -1.0);
+           last > 0 ? last - t0 : -1.0, first, last);
     return 0;
 }

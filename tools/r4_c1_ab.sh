@@ -12,7 +12,7 @@ for r in $(seq 1 "$rounds"); do
   for shape in "1 1" "1 2" "4 3"; do
     set -- $shape
     timeout -k 10 200 python "$R/tools/loopback/c1_bench.py" --threads "$1" --blasters "$2" --seconds 3 \
-      --exe "r2=$R/tools/ab_r2/bin/statsd-router-mi355x" --var "sync:SR_DT_SYNC=1" --var "noyield:SR_DT_YIELD=0" \
+      --exe "r2=$R/tools/ab_r2/bin/statsd-router-mi355x" --var "y4:SR_DT_YIELD=4,SR_DT_YIELD_S=0" --var "noyield:SR_DT_YIELD_S=0" \
       >> "$out" 2>> "$R/gpurun_out/c1_ab_${tag}.err" || exit 1
   done
 done
