@@ -60,6 +60,8 @@ constexpr int kMtuWindow = kMtuCap / (int)SR_MIN_LINE_LENGTH + 1;   // a packet 
 constexpr int kMtuX = kMtuCap + 1;               // incoming fills 0..1450
 constexpr uint32_t kMtuNone = 0xFFFFFFFFu;
 constexpr uint16_t kMtuEnd = 0xFFFFu;
+constexpr int kMtuP0 = 256;                      // prefix sums kept per chunk for the first line over the cap
+static_assert(kMtuWindow <= kMtuP0, "the incoming packet closes within a chunk's first kMtuP0 lines");
 
 constexpr int kMtuMaxBatches = 32;
 
@@ -99,7 +101,8 @@ struct MtuLaunch {
     uint32_t *closed;                  // [nb][nds] packets closed per shard
     uint64_t *table;                   // [chunks][kMtuX]
     uint8_t *nx;                       // [chunks][kMtuChunk] next(i) - i per line (mtu_table -> mtu_emit)
-    uint32_t *gp;                      // [chunks][kMtuChunk] the chunks' length prefix sums (mtu_table -> mtu_emit)
+    uint16_t *plen;                    // [chunks][kMtuChunk] bytes of the packet a line starts (mtu_table -> mtu_emit)
+    uint32_t *gp0;                     // [chunks][kMtuP0 + 1] the first prefix sums and the chunk's bytes
     uint64_t *dbg;                     // SR_MTU_STAMPS developer builds only: 8 timestamps per chunk
     MtuBatchArg b[kMtuMaxBatches];
 };
@@ -122,7 +125,8 @@ struct MtuParams {
     uint32_t *chunk_shard;
     uint64_t *table;
     uint8_t *nx;
-    uint32_t *gp;
+    uint16_t *plen;
+    uint32_t *gp0;
     uint32_t *chunk_entry;    // incoming fill | first line over the cap from it << 16
     uint32_t *chunk_open;     // kMtuNone: the incoming packet began before the batch
     uint32_t *chunk_pk;
@@ -152,7 +156,8 @@ __device__ __forceinline__ MtuParams mtu_view(const MtuLaunch &L, uint32_t bi) {
     p.chunk_shard = L.chunk_shard + a.chunk0;
     p.table = L.table + (size_t)a.chunk0 * kMtuX;
     p.nx = L.nx + (size_t)a.chunk0 * kMtuChunk;
-    p.gp = L.gp + (size_t)a.chunk0 * kMtuChunk;
+    p.plen = L.plen + (size_t)a.chunk0 * kMtuChunk;
+    p.gp0 = L.gp0 + (size_t)a.chunk0 * (kMtuP0 + 1);
     p.chunk_entry = L.chunk_entry + a.chunk0;
     p.chunk_open = L.chunk_open + a.chunk0;
     p.chunk_pk = L.chunk_pk + a.chunk0;
@@ -304,10 +309,21 @@ __global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuLaunch L) {
     if (tid == 1023) {
         p.chunk_first[p.nds] = run;
         p.counts[1] = p.key_start[p.nds];
+        if (run == 0) p.counts[0] = 0;   // (mtu_emit<WALK> writes it otherwise)
     }
+    // the pending bytes of shards without lines (mtu_emit<WALK> writes the others')
+    for (uint32_t s = tid; s < p.nds; s += 1024)
+        if (p.key_start[s + 1] == p.key_start[s]) {
+            const uint32_t x = p.fill_in ? min((uint32_t)p.fill_in[s], (uint32_t)kMtuCap) : 0u;
+            p.fill_out[s] = mtu_dropped(p, s) ? 0 : (uint16_t)x;
+        }
 }
 
-__global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_scatter_kernel(MtuLaunch L) {
+#ifndef SR_SCATTER_WPE
+#define SR_SCATTER_WPE 1   // minimum waves per SIMD the scatter kernel is compiled for (developer A/B)
+#endif
+__global__ __launch_bounds__(64 * kMtuSortWaves) __attribute__((amdgpu_waves_per_eu(SR_SCATTER_WPE)))
+void mtu_scatter_kernel(MtuLaunch L) {
     extern __shared__ uint32_t lds_pos[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t g = blockIdx.x * kMtuSortWaves + (uint32_t)wave;
@@ -354,14 +370,6 @@ __global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_scatter_kernel(MtuLaun
 }
 
 // ---- packing: per-chunk next-fit tables -------------------------------------------------------
-// LDS of the two chunk kernels, kept apart so that each holds only what it reads (4096-line chunks:
-// 32 KiB, five workgroups per CU instead of three; 20 KiB for emit; half that for 2048-line chunks).
-// The prefix scan's wave sums borrow ld / nx.
-template <int CH>
-struct MtuTableSmem {
-    uint32_t P[CH];      // inclusive prefix of the chunk's line lengths
-    uint32_t ld[CH];     // last packet start reached from here << 16 | packets closed on the way
-};
 #ifndef SR_MTU_HOP
 #define SR_MTU_HOP 16
 #endif
@@ -372,6 +380,7 @@ struct MtuEmitSmem {
     uint16_t J[CH];               // kMtuHop packet starts ahead on the chain (kMtuEnd: it ends first)
     uint16_t anchor[CH / kMtuHop + 2];
     uint32_t nanchor;
+    uint32_t bc[4];               // WALK: the chunk's incoming fill, first line over the cap, open, first slot
 };
 
 struct MtuChunk {
@@ -404,7 +413,7 @@ __device__ __forceinline__ uint32_t mtu_first_over(const uint32_t *P, uint32_t l
 // running sum carried across the wave's 16 rows by DPP scans; one barrier for the wave offsets.
 template <int CH, int NT = kMtuBlock>
 __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuChunk &ck, uint32_t *P,
-                                                 uint32_t *wsum, uint32_t *gP = nullptr) {
+                                                 uint32_t *wsum) {
     constexpr int kMtuPer = CH / NT;
     if (SR_MTU_SKIP & 16) {
         for (uint32_t i = threadIdx.x; i < (uint32_t)CH; i += NT) P[i] = 64u * (i + 1);
@@ -432,149 +441,152 @@ __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuCh
     for (int w = 0; w < wave; ++w) add += wsum[w];
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) P[base + 64u * k] = v[k] + add;
-    if (gP) {   // the emit kernel's copy (coalesced rows; past the chunk's lines unused)
-#pragma unroll
-        for (int k = 0; k < kMtuPer; ++k) gP[base + 64u * k] = v[k] + add;
-    }
     __syncthreads();
 }
 
-// next(i) = the first line that no longer fits a packet starting at line i (kMtuEnd: none in the
-// chunk), for lines tid + 256 k: a fixed 8-step search over the 256 lines after i (a packet holds
-// fewer than 242), the 16 searches of a thread independent, neighbouring lanes on neighbouring
-// words. f(i, next) stores the result.
-template <int CH, int NT, typename F>
-__device__ __forceinline__ void mtu_chunk_next(const uint32_t *P, uint32_t cnt, F f) {
-    constexpr int kMtuPer = CH / NT;
-    if (SR_MTU_SKIP & 8) {
-        for (uint32_t i = threadIdx.x; i < cnt; i += NT) f(i, i + 22 < cnt ? (uint16_t)(i + 22) : kMtuEnd);
-        return;
-    }
-    // (every LDS read unconditional, at a clamped index: a read under a per-lane condition became
-    // a branch with its own wait, and the 16 searches ran one after another)
-    const uint32_t total = P[cnt - 1];
-    uint32_t lo[kMtuPer], lim[kMtuPer];
-#pragma unroll
-    for (int k = 0; k < kMtuPer; ++k) {
-        const uint32_t i = threadIdx.x + (uint32_t)k * NT;
-        lo[k] = i;   // P[i] <= lim: a line alone always fits
-        const uint32_t pm = P[min(i ? i - 1 : 0u, cnt - 1)];
-        lim[k] = pm * (uint32_t)(i != 0) + (uint32_t)kMtuCap;
-    }
-    // past the chunk the clamped read gives P[cnt - 1] = total, which is over lim unless no line
-    // closes the packet (next = kMtuEnd below, lo unused): no bounds test, so no branch
-#if SR_MTU_NEXT_GUESS
-    // Row 0 by the search; every later row first tries row 0's offset (exact for lines of one
-    // length), and a wave searches a row only if one of its lanes missed.
-#pragma unroll
-    for (uint32_t step = 128; step; step >>= 1) {
-        const uint32_t t = lo[0] + step;
-        const uint32_t pt = P[min(t, cnt - 1)];
-        lo[0] = pt <= lim[0] ? t : lo[0];
-    }
-    const uint32_t d0 = lo[0] - threadIdx.x;
-    bool miss[kMtuPer];
-#pragma unroll
-    for (int k = 1; k < kMtuPer; ++k) {   // the guesses: two reads per row, all rows at once
-        const uint32_t g = min(lo[k] + d0, cnt - 1);
-        const uint32_t pg = P[g], pn = P[min(g + 1, cnt - 1)];
-        miss[k] = !(pg <= lim[k] && (g + 1 >= cnt || pn > lim[k]));
-        lo[k] = g;
-    }
-#pragma unroll
-    for (int k = 1; k < kMtuPer; ++k) {
-        if (__ballot(miss[k])) {
-            lo[k] = threadIdx.x + (uint32_t)k * NT;
-#pragma unroll
-            for (uint32_t step = 128; step; step >>= 1) {
-                const uint32_t t = lo[k] + step;
-                const uint32_t pt = P[min(t, cnt - 1)];
-                lo[k] = pt <= lim[k] ? t : lo[k];
-            }
-        }
-    }
-#else
-#pragma unroll
-    for (uint32_t step = 128; step; step >>= 1) {
-#pragma unroll
-        for (int k = 0; k < kMtuPer; ++k) {
-            const uint32_t t = lo[k] + step;
-            const uint32_t pt = P[min(t, cnt - 1)];
-            lo[k] = pt <= lim[k] ? t : lo[k];
-        }
-    }
-#endif
-#pragma unroll
-    for (int k = 0; k < kMtuPer; ++k) {
-        const uint32_t i = threadIdx.x + (uint32_t)k * NT;
-        if (i < cnt) f(i, total <= lim[k] ? kMtuEnd : (uint16_t)(lo[k] + 1));
-    }
-}
-
 // table[c][x] = (first line over the cap << 48) | (packets closed << 32) | (last packet start << 16,
-// 0xFFFF = none) | fill after (a chunk closes at most kMtuChunk + 1 packets: 16 bits)
+// 0xFFFF = none) | fill after (a chunk closes at most kMtuChunk + 1 packets: 16 bits).
+// One array of LDS: the prefix sums, overwritten by the doubling words once next() is in registers
+// (its searches done), plus the first kMtuP0 prefix sums (the incoming fill's first line over the cap
+// is always among them) and one table entry per possible first line. 4096-line chunks: 19 KiB of
+// LDS and at most 64 VGPRs, so that eight workgroups share a CU and every chunk of a C2 launch is
+// resident at once (round 3's kernel held P and the doubling words apart: 32 KiB, five per CU).
+// next() and the doubling run in halves of the thread's rows to stay within the registers. For
+// mtu_emit: next(i) - i and the bytes of the packet line i would start (both per line), the first
+// prefix sums and the chunk's bytes.
+template <int CH>
+struct MtuTableSmem {
+    uint32_t P[CH];        // inclusive prefix of the chunk's line lengths, then the doubling words:
+                           // last packet start reached from here << 16 | packets closed on the way
+    uint32_t P0[kMtuP0];   // P[0 .. kMtuP0 - 1]
+    uint64_t e[kMtuP0];    // per first line j: packets closed << 32 | last start << 16 | fill out
+    uint32_t wsum[16];     // the prefix scan's wave sums
+};
+
 template <int CH, int NT = kMtuTableBlock>
-__global__ __launch_bounds__(NT) void mtu_table_kernel(MtuLaunch L) {
+__global__ __launch_bounds__(NT, 8) void mtu_table_kernel(MtuLaunch L) {
     constexpr int kMtuPer = CH / NT;
+    constexpr int kHalf = kMtuPer >= 16 ? kMtuPer / 2 : kMtuPer;   // rows per pass
+    static_assert(NT >= kMtuP0, "one thread per kept prefix sum");
     __shared__ MtuTableSmem<CH> sm;
     MtuChunk ck;
     const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.chunk0; });
     const MtuParams p = mtu_view(L, bi);
     const uint32_t c = blockIdx.x - L.b[bi].chunk0;
     if (!mtu_chunk_of(p, c, ck)) return;
-    const int tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x;
     mtu_stamp(L, blockIdx.x, 0);
-    mtu_chunk_prefix<CH, NT>(p, ck, sm.P, sm.ld, p.gp + (size_t)c * kMtuChunk);
+    mtu_chunk_prefix<CH, NT>(p, ck, sm.P, sm.wsum);
     mtu_stamp(L, blockIdx.x, 1);
+    const uint32_t cnt = ck.cnt, total = sm.P[cnt - 1];
+    uint32_t *gp0 = p.gp0 + (size_t)c * (kMtuP0 + 1);
+    if (tid < (uint32_t)kMtuP0) {
+        const uint32_t v = sm.P[min(tid, cnt - 1)];
+        sm.P0[tid] = v;
+        gp0[tid] = v;
+    }
+    if (tid == 0) gp0[kMtuP0] = total;
+    // next(i) for rows k (lines tid + NT k), from the inclusive prefix P: the last line lo that still
+    // fits a packet starting at i (P[lo] <= lim = P[i - 1] + cap), next = lo + 1 (kMtuEnd: the
+    // chunk's end comes first), by a fixed 8-step search over the 256 lines after i (a packet holds
+    // fewer than 242). Every LDS read is unconditional at a clamped index (a read under a per-lane
+    // condition becomes a branch with its own wait); past the chunk the clamped read gives
+    // P[cnt - 1] = total. kHalf rows at a time (registers), results packed two per register.
+    uint32_t nxp[(kMtuPer + 1) / 2];
     uint8_t *gnx = p.nx + (size_t)c * kMtuChunk;
-    mtu_chunk_next<CH, NT>(sm.P, ck.cnt, [&](uint32_t i, uint16_t nxt) {
-        sm.ld[i] = nxt == kMtuEnd ? i << 16 : ((uint32_t)nxt << 16) | 1u;
-        if (!(SR_MTU_SKIP & 32)) gnx[i] = nxt == kMtuEnd ? 0 : (uint8_t)(nxt - i);   // for mtu_emit
-    });
-    for (uint32_t i = ck.cnt + (uint32_t)tid; i < (uint32_t)CH; i += NT) sm.ld[i] = i << 16;   // self loops
+    uint16_t *gpl = p.plen + (size_t)c * kMtuChunk;
+#pragma unroll
+    for (int h = 0; h < kMtuPer; h += kHalf) {
+        uint32_t lo[kHalf], lim[kHalf];
+#pragma unroll
+        for (int k = 0; k < kHalf; ++k) {
+            const uint32_t i = tid + (uint32_t)(h + k) * NT;
+            lo[k] = i;   // P[i] <= lim: a line alone always fits
+            const uint32_t pm = sm.P[min(i ? i - 1 : 0u, cnt - 1)];
+            lim[k] = pm * (uint32_t)(i != 0) + (uint32_t)kMtuCap;
+        }
+#pragma unroll
+        for (uint32_t step = 128; step; step >>= 1) {
+#pragma unroll
+            for (int k = 0; k < kHalf; ++k) {
+                const uint32_t t = lo[k] + step;
+                lo[k] = sm.P[min(t, cnt - 1)] <= lim[k] ? t : lo[k];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < kHalf; ++k) {
+            const uint32_t i = tid + (uint32_t)(h + k) * NT;
+            const bool end = total <= lim[k];
+            const uint32_t nxt = (i >= cnt || end) ? (uint32_t)kMtuEnd : lo[k] + 1;
+            // the packet from line i: up to next(i) (its last line lo), or to the chunk's end
+            const uint32_t pe = end ? total : sm.P[min(lo[k], cnt - 1)];
+            if (i < cnt) {
+                gnx[i] = nxt == kMtuEnd ? 0 : (uint8_t)(nxt - i);
+                gpl[i] = (uint16_t)(pe - (lim[k] - (uint32_t)kMtuCap));
+            }
+            const int r = h + k;
+            if (r & 1) nxp[r >> 1] |= nxt << 16;
+            else nxp[r >> 1] = nxt;
+        }
+    }
+    __syncthreads();   // every search's reads of P done: the array becomes the doubling words
+#pragma unroll
+    for (int k = 0; k < kMtuPer; ++k) {
+        const uint32_t i = tid + (uint32_t)k * NT;
+        const uint32_t nxt = (nxp[k >> 1] >> ((k & 1) * 16)) & 0xFFFFu;
+        sm.P[i] = nxt == kMtuEnd ? i << 16 : (nxt << 16) | 1u;   // past the chunk: self loops
+    }
     __syncthreads();
     mtu_stamp(L, blockIdx.x, 2);
-    const uint32_t total = sm.P[ck.cnt - 1];
-    // pointer doubling: ld -> the last packet start of the chain and the packets closed on it.
-    // A chain closes at most 2 * total / (cap + 1) + 1 packets (two consecutive closed packets
-    // exceed the cap together), so that many jumps suffice.
-    const uint32_t kb = min(ck.cnt, 2u * total / (uint32_t)(kMtuCap + 1) + 2u);
-    // In place, one barrier per round: a neighbour read mid-round has jumped at least as far as
-    // at the round's start, so after r rounds every jump spans >= 2^r starts (or ends the chain).
-    for (uint32_t span = 1; !(SR_MTU_SKIP & 1) && span < kb; span <<= 1) {
-        uint32_t v[kMtuPer], w[kMtuPer];   // every line (past the chunk: self loops), loads first
+    // pointer doubling: ld -> the last packet start of the chain and the packets closed on it. A
+    // chain closes at most 2 * total / (cap + 1) + 1 packets (two consecutive closed packets exceed
+    // the cap together), so that many jumps suffice. In place, one barrier per round: a neighbour
+    // read mid-round has jumped at least as far as at the round's start, so after r rounds every
+    // jump spans >= 2^r starts (or ends the chain).
+    const uint32_t kb = min(cnt, 2u * total / (uint32_t)(kMtuCap + 1) + 2u);
+    for (uint32_t span = 1; span < kb; span <<= 1) {
 #pragma unroll
-        for (int k = 0; k < kMtuPer; ++k) v[k] = sm.ld[(uint32_t)tid + (uint32_t)k * NT];
+        for (int h = 0; h < kMtuPer; h += kHalf) {
+            uint32_t v[kHalf], w[kHalf];
 #pragma unroll
-        for (int k = 0; k < kMtuPer; ++k) w[k] = sm.ld[v[k] >> 16];
+            for (int k = 0; k < kHalf; ++k) v[k] = sm.P[tid + (uint32_t)(h + k) * NT];
 #pragma unroll
-        for (int k = 0; k < kMtuPer; ++k)
-            sm.ld[(uint32_t)tid + (uint32_t)k * NT] = (w[k] & 0xFFFF0000u) | ((v[k] + w[k]) & 0xFFFFu);
+            for (int k = 0; k < kHalf; ++k) w[k] = sm.P[v[k] >> 16];
+#pragma unroll
+            for (int k = 0; k < kHalf; ++k)
+                sm.P[tid + (uint32_t)(h + k) * NT] = (w[k] & 0xFFFF0000u) | ((v[k] + w[k]) & 0xFFFFu);
+        }
         __syncthreads();
     }
     mtu_stamp(L, blockIdx.x, 3);
+    // one entry per possible first line j (< 242 <= kMtuP0): the fill out is the bytes of the open
+    // packet from the last start l, the packet length stored above for l (this workgroup's own
+    // global writes, ordered before the barriers since)
+    const uint32_t hi = min(cnt, (uint32_t)kMtuWindow);
+    if (tid < hi) {
+        const uint32_t v = sm.P[tid], l = v >> 16;
+        sm.e[tid] = ((uint64_t)(1u + (v & 0xFFFFu)) << 32) | ((uint64_t)l << 16) | gpl[l];
+    }
+    __syncthreads();
     // incoming fills x0 .. x0 + per - 1 per thread: the first line over the cap moves down with x
     constexpr uint32_t per = (kMtuX + NT - 1) / NT;
-    const uint32_t hi = min(ck.cnt, (uint32_t)kMtuWindow);
     uint64_t *row = p.table + (size_t)c * kMtuX;
-    const uint32_t x0 = (uint32_t)tid * per;
+    const uint32_t x0 = tid * per;
     uint32_t j = 0;
     bool first = true;
-    for (uint32_t x = x0; !(SR_MTU_SKIP & 2) && x < x0 + per && x < (uint32_t)kMtuX; ++x) {
+    for (uint32_t x = x0; x < x0 + per && x < (uint32_t)kMtuX; ++x) {
         uint64_t e;
         if (x + total <= (uint32_t)kMtuCap) {
             e = (0xFFFFull << 16) | (x + total);
         } else {
             const uint32_t lim = (uint32_t)kMtuCap - x;
             if (first) {
-                j = mtu_first_over(sm.P, 0, hi - 1, lim);
+                j = mtu_first_over(sm.P0, 0, hi - 1, lim);
                 first = false;
             } else {
-                while (j > 0 && sm.P[j - 1] > lim) --j;
+                while (j > 0 && sm.P0[j - 1] > lim) --j;
             }
-            const uint32_t v = sm.ld[j], l = v >> 16;
-            e = ((uint64_t)j << 48) | ((uint64_t)(1u + (v & 0xFFFFu)) << 32) | ((uint64_t)l << 16) |
-                (total - (l ? sm.P[l - 1] : 0u));
+            e = ((uint64_t)j << 48) | sm.e[j];
         }
         row[x] = e;
     }
@@ -638,11 +650,19 @@ __device__ __forceinline__ void mtu_put(const MtuParams &p, uint32_t k, uint32_t
 // The chunk's packet chain (the first line that does not fit the incoming packet, then next()):
 // four rounds of pointer doubling give every line the start kMtuHop packets ahead (J); one thread
 // walks the chain by those hops, leaving an anchor every kMtuHop packets; then every anchor's
-// thread walks its kMtuHop packets by next() (LDS), loads their prefix sums (the table kernel's
-// global copy, all loads in flight together) and writes their descriptors (rank = 16 q + step).
+// thread walks its kMtuHop packets by next() (LDS), loads their lengths (the table kernel's bytes per
+// packet start, all loads in flight together) and writes their descriptors (rank = 16 q + step).
 // The chain's first line j comes with the chunk's incoming fill (mtu_chain, from the table): no
 // prefix sums in LDS, so that every chunk of a launch is resident at once.
-template <int CH>
+//
+// WALK (a batch of at most 64 shards): no mtu_chain kernel. Wave 0 of every chunk walks the tables
+// itself, one lane per shard of the batch, all lanes at once: a lane before the chunk's shard its
+// whole chain from the shard's fill_in (the shard's packet total), the chunk's own shard's lane up to
+// the chunk (its incoming fill, where its open packet began, the packets closed before it). The
+// chunk's first descriptor is the totals of the shards before it plus its own shard's closed
+// packets. A shard's last chunk writes its fill out, the batch's last chunk the batch's packet count
+// (shards without lines: mtu_scan).
+template <int CH, bool WALK>
 __global__ __launch_bounds__(kMtuBlock, 8) void mtu_emit_kernel(MtuLaunch L) {   // 8 waves per SIMD: every chunk resident
     constexpr int kMtuPer = CH / kMtuBlock;
     __shared__ MtuEmitSmem<CH> sm;
@@ -653,10 +673,65 @@ __global__ __launch_bounds__(kMtuBlock, 8) void mtu_emit_kernel(MtuLaunch L) {  
     if (!mtu_chunk_of(p, c, ck)) return;
     mtu_stamp(L, blockIdx.x, 5);
     const int tid = threadIdx.x;
-    const uint32_t *gP = p.gp + (size_t)c * kMtuChunk;
-    const uint32_t xe = p.chunk_entry[c], open = p.chunk_open[c], k0 = p.chunk_pk[c];
-    const uint32_t x = xe & 0xFFFFu, j = xe >> 16;
-    const uint32_t total = gP[ck.cnt - 1];
+    const uint32_t *gp0 = p.gp0 + (size_t)c * (kMtuP0 + 1);
+    const uint16_t *gpl = p.plen + (size_t)c * kMtuChunk;
+    // next(i) - i as mtu_table stored it (16 bytes per thread), issued before the walk
+    constexpr int kNxPer = (CH / 16 + kMtuBlock - 1) / kMtuBlock;
+    uint4 nxv[kNxPer];
+#pragma unroll
+    for (int k = 0; k < kNxPer; ++k) {
+        const uint32_t v = (uint32_t)tid + (uint32_t)k * kMtuBlock;
+        nxv[k] = v * 16 < ck.cnt ? reinterpret_cast<const uint4 *>(p.nx + (size_t)c * kMtuChunk)[v] : make_uint4(0, 0, 0, 0);
+    }
+    uint32_t x, j, open, k0;
+    if constexpr (WALK) {
+        if (tid < 64) {
+            const uint32_t s = (uint32_t)tid;
+            uint32_t tot = 0, xs = 0, os = kMtuNone, cs = 0;
+            uint64_t es = 0;
+            if (s <= ck.shard) {
+                xs = p.fill_in ? min((uint32_t)p.fill_in[s], (uint32_t)kMtuCap) : 0u;
+                const uint32_t c0 = p.chunk_first[s];
+                const uint32_t c1 = s == ck.shard ? c + 1 : min(p.chunk_first[s + 1], p.max_chunks);
+                for (uint32_t cc = c0; cc < c1; ++cc) {
+                    const uint64_t e = p.table[(size_t)cc * kMtuX + xs];
+                    if (cc == c) {   // this chunk's own entry, at its incoming fill
+                        es = e;
+                        break;
+                    }
+                    const uint32_t cl = (uint32_t)(e >> 32) & 0xFFFFu;
+                    if (cl) {
+                        cs += cl;
+                        os = p.key_start[s] + (cc - c0) * p.chunk_lines + (uint32_t)((e >> 16) & 0xFFFFu);
+                    }
+                    xs = (uint32_t)(e & 0xFFFFu);
+                }
+                if (s < ck.shard) tot = cs + (c1 > c0 ? 1u : 0u);
+            }
+            const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_add32(tot), 63);
+            if (s == ck.shard) {
+                sm.bc[0] = xs;
+                sm.bc[1] = (uint32_t)(es >> 48);
+                sm.bc[2] = os;
+                sm.bc[3] = base + cs;
+                const uint32_t cl = (uint32_t)(es >> 32) & 0xFFFFu;
+                if (ck.last) p.fill_out[s] = mtu_dropped(p, s) ? 0 : (uint16_t)(es & 0xFFFFu);
+                if (c + 1 == min(p.chunk_first[p.nds], p.max_chunks)) p.counts[0] = base + cs + cl + 1u;
+            }
+        }
+        __syncthreads();
+        x = sm.bc[0];
+        j = sm.bc[1];
+        open = sm.bc[2];
+        k0 = sm.bc[3];
+    } else {
+        const uint32_t xe = p.chunk_entry[c];
+        x = xe & 0xFFFFu;
+        j = xe >> 16;
+        open = p.chunk_open[c];
+        k0 = p.chunk_pk[c];
+    }
+    const uint32_t total = gp0[kMtuP0];
     const uint32_t carry = open == kMtuNone ? x : 0u;        // pending bytes from before the batch
     const uint32_t start = open == kMtuNone ? p.key_start[ck.shard] : open;
     if (x + total <= (uint32_t)kMtuCap) {   // no line of the chunk closes a packet: the incoming one stays open
@@ -665,14 +740,14 @@ __global__ __launch_bounds__(kMtuBlock, 8) void mtu_emit_kernel(MtuLaunch L) {  
         return;
     }
     if (tid == 0)   // the incoming packet closes before line j
-        mtu_put(p, k0, start, ck.pos0 + j - start, ck.shard, x - carry + (j ? gP[j - 1] : 0u), carry, 0u);
-    // next(i) - i as mtu_table stored it (16 bytes per thread), then J: next(i), doubled four times
-    // (exact: all reads of a round before its writes)
+        mtu_put(p, k0, start, ck.pos0 + j - start, ck.shard, x - carry + (j ? gp0[j - 1] : 0u), carry, 0u);
+    // next(i) - i into LDS, then J: next(i), doubled four times (exact: all reads of a round before
+    // its writes)
 #pragma unroll
-    for (uint32_t v = (uint32_t)tid; v * 16 < (uint32_t)CH; v += kMtuBlock)
-        reinterpret_cast<uint4 *>(sm.nx)[v] = v * 16 < ck.cnt
-                                                  ? reinterpret_cast<const uint4 *>(p.nx + (size_t)c * kMtuChunk)[v]
-                                                  : make_uint4(0, 0, 0, 0);
+    for (int k = 0; k < kNxPer; ++k) {
+        const uint32_t v = (uint32_t)tid + (uint32_t)k * kMtuBlock;
+        if (v * 16 < (uint32_t)CH) reinterpret_cast<uint4 *>(sm.nx)[v] = nxv[k];
+    }
     __syncthreads();
     mtu_stamp(L, blockIdx.x, 6);
     uint16_t jv[kMtuPer];
@@ -708,7 +783,7 @@ __global__ __launch_bounds__(kMtuBlock, 8) void mtu_emit_kernel(MtuLaunch L) {  
     __syncthreads();
     const uint32_t na = sm.nanchor;
     for (uint32_t q = (uint32_t)tid; q < na; q += kMtuBlock) {
-        // the anchor's packets: starts and ends from next() in LDS, then every prefix sum they need
+        // the anchor's packets: starts and ends from next() in LDS, then every packet's length
         // loaded before the first descriptor store (a store waits for the loads issued before it)
         // (consecutive packets: each starts where the one before it ends)
         uint32_t bs[kMtuHop];
@@ -727,19 +802,17 @@ __global__ __launch_bounds__(kMtuBlock, 8) void mtu_emit_kernel(MtuLaunch L) {  
                 a += d;
             }
         }
-        uint32_t pb[kMtuHop];
-        const uint32_t pl = gP[a0 ? a0 - 1u : 0u];   // unconditional (clamped) load
-        const uint32_t pa0 = a0 ? pl : 0u;
+        uint32_t pl[kMtuHop];
 #pragma unroll
-        for (int step = 0; step < kMtuHop; ++step) pb[step] = gP[bs[step] - 1u];   // all in flight together
-        uint32_t s0 = a0, p0 = pa0;
+        for (int step = 0; step < kMtuHop; ++step)   // unconditional (clamped) loads, all in flight together
+            pl[step] = gpl[min(step ? bs[step - 1] : a0, ck.cnt - 1)];
+        uint32_t s0 = a0;
 #pragma unroll
         for (int step = 0; step < kMtuHop; ++step) {
             if (step < ns)
-                mtu_put(p, k0 + 1 + q * kMtuHop + (uint32_t)step, ck.pos0 + s0, bs[step] - s0, ck.shard, pb[step] - p0, 0u,
+                mtu_put(p, k0 + 1 + q * kMtuHop + (uint32_t)step, ck.pos0 + s0, bs[step] - s0, ck.shard, pl[step], 0u,
                         (is_open && ck.last && step == ns - 1) ? 1u : 0u);   // the chain's open packet
             s0 = bs[step];
-            p0 = pb[step];
         }
     }
     mtu_stamp(L, blockIdx.x, 7);

@@ -93,7 +93,9 @@ enum : unsigned {
 
 // Product kernel variants (same records, bit for bit): KV_SEGMENTS lays a tile of mixed line
 // lengths out one lane per 64-byte name segment (route_host.hpp picks the variant per launch).
-enum : unsigned { KV_UNIFORM = 0u, KV_SEGMENTS = 4194304u };
+// KV_ALIVE: a launch whose every shard is alive (the shard is h % N): no probe, overlay, deferral or
+// probed-dead marks in the kernel, and none of their registers.
+enum : unsigned { KV_UNIFORM = 0u, KV_SEGMENTS = 4194304u, KV_ALIVE = 268435456u };
 
 constexpr uint64_t ipow(uint64_t b, unsigned e) {
     uint64_t r = 1;
@@ -1506,12 +1508,13 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 uint32_t route;
                 if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
                 else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
+                else if (ABL & KV_ALIVE) route = p.nds ? mod_magic(h, p.magic_n, p.nds) : SR_ROUTE_ALL_DEAD;   // :145
                 else route = probe_shard(h, p, nullptr, sm.img, nullptr, p.defer != 0,
                                          p.mark ? sm.img : nullptr);                                // :145
                 // a probe past its first two picks goes to probe_defer_kernel: the record is marked
                 // pending and the hash kept by record index (no counter: same-address atomics from
                 // every wave serialise at the memory side)
-                const bool deferred = route == kRouteDefer;
+                const bool deferred = !(ABL & KV_ALIVE) && route == kRouteDefer;
                 if (deferred) route = kRoutePending;
                 sr_record r;
                 r.offset = (uint32_t)(T0 + s);
@@ -1528,7 +1531,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 const uint32_t rec = base + (uint32_t)j;
                 if (rec < bd.max_records) {
                     if (deferred) bd.dhash[rec] = h;
-                    if (route == kRoutePending && !deferred) {
+                    if (!(ABL & KV_ALIVE) && route == kRoutePending && !deferred) {
                         const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
                         if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
                     }
@@ -1796,21 +1799,21 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     in.sx = (ABL & ABL_AGENT_GRANULES) ? 0ull
                                        : __hip_atomic_load(&p.ctl->scan_xcc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < S::kPowWords) ((uint32_t *)&sm.kp_lo[0])[tid] = kp;   // kp_lo | kp_hi | kp_inv are contiguous
-    if (p.dead && p.dead < p.nds && tid < 4 * (int)kMagicLds) {   // the probe's first reciprocals (probe_shard)
+    if (!(ABL & KV_ALIVE) && p.dead && p.dead < p.nds && tid < 4 * (int)kMagicLds) {   // the probe's first reciprocals (probe_shard)
         const uint32_t e = (uint32_t)tid >> 2;   // divisor nds - e >= 1: entries e < nds only
         if (e < p.nds) sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)&p.magic[p.nds - e])[tid & 3];
     }
-    if (p.dead && p.dead < p.nds && p.nds <= 64 * kAliveLds && tid >= (int)kAliveRow0 &&
+    if (!(ABL & KV_ALIVE) && p.dead && p.dead < p.nds && p.nds <= 64 * kAliveLds && tid >= (int)kAliveRow0 &&
         (uint32_t)tid < kAliveRow0 + 2 * ((p.nds + 63) / 64))   // the alive words (probe_shard)
         sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)p.alive)[tid - kAliveRow0];
-    if (p.mark && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
+    if (!(ABL & KV_ALIVE) && p.mark && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
         sm.img[(uint32_t)tid * 17 + 16] = 0u;
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
     uint64_t nlm, clm;
     uint32_t c_in;
     tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
     tile_lines<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
-    if (p.mark && p.b[bi].probed_dead) {   // MARK_LDS: the dead shards this tile's probes visited
+    if (!(ABL & KV_ALIVE) && p.mark && p.b[bi].probed_dead) {   // MARK_LDS: the dead shards this tile's probes visited
         wg_barrier();
         if ((uint32_t)tid < p.nwords) {   // the tile's slot, ORed by probe_defer_kernel (no atomics)
             const uint32_t lo = sm.img[(kMarkRow0 + 2 * (uint32_t)tid) * 17 + 16];

@@ -44,7 +44,7 @@ struct sr_ctx {
     uint32_t mtu_ntiles, mtu_chunks;
     uint32_t *d_mtu_tiles, *d_mtu_keys, *d_mtu_chunks;
     uint64_t *d_mtu_table;
-    uint32_t *d_mtu_gp;    // the chunks' prefix sums, chunks * kMtuChunk entries
+    uint32_t *d_mtu_gp;    // per chunk: bytes per packet start (kMtuChunk u16), then the first prefix sums
     // buffers of sr_route_pack_batch
     sr_record *d_sorted;
     size_t d_sorted_cap;
@@ -74,13 +74,20 @@ static void free_ptr(void *p) { (void)hipFree(p); }
 #define SR_CHUNK_ABL 0u   // developer ablation builds of route_chunk_kernel only (chunk_kernel.hpp)
 #endif
 
-// The product launches KV_UNIFORM or KV_SEGMENTS (identical records; DeviceState::choose_segments
-// picks by the lane-layout policy). Ablation variants (records wrong by design in some of them)
+// The product launches KV_UNIFORM, KV_SEGMENTS or KV_CHUNKS (identical records;
+// DeviceState::choose_segments picks by the lane-layout policy). Ablation variants (records wrong by design in some of them)
 // exist only in builds made with -DSR_ABLATION_VARIANTS (`make VARIANTS=1`, developer A/B runs;
 // never the shipped library): SR_VARIANT in the environment then selects one.
 static int launch_product(DeviceState &ds, const RouteParams &p, hipStream_t stream) {
     const bool seg = ds.choose_segments(stream);
-    if (ds.last_layout == SR_LAYOUT_CHUNKS) return launch_route<kBlock, KV_CHUNKS | SR_CHUNK_ABL>(ds, p, stream);
+    if (ds.last_layout == SR_LAYOUT_CHUNKS) {
+        if (ds.dead == 0) return launch_route<kBlock, KV_CHUNKS | KV_ALIVE | SR_CHUNK_ABL>(ds, p, stream);
+        return launch_route<kBlock, KV_CHUNKS | SR_CHUNK_ABL>(ds, p, stream);
+    }
+    if (ds.dead == 0) {   // every shard alive: the variants without the probe
+        if (seg) return launch_route<kBlock, KV_SEGMENTS | KV_ALIVE>(ds, p, stream);
+        return launch_route<kBlock, KV_UNIFORM | KV_ALIVE>(ds, p, stream);
+    }
     if (seg) return launch_route<kBlock, KV_SEGMENTS>(ds, p, stream);
     return launch_route<kBlock, KV_UNIFORM>(ds, p, stream);
 }
@@ -371,7 +378,9 @@ static int mtu_reserve(sr_ctx *c, uint32_t tiles, uint32_t chunks, uint32_t nb) 
         // the tables, then next(i) - i of every line of every chunk
         if (hipMalloc(&c->d_mtu_table, (size_t)chunks * (kMtuX * sizeof(uint64_t) + kMtuChunk) + 16) != hipSuccess)
             return -ENOMEM;
-        if (hipMalloc(&c->d_mtu_gp, (size_t)chunks * kMtuChunk * sizeof(uint32_t)) != hipSuccess) return -ENOMEM;
+        if (hipMalloc(&c->d_mtu_gp, (size_t)chunks * (kMtuChunk * sizeof(uint16_t) + (kMtuP0 + 1) * sizeof(uint32_t))) !=
+            hipSuccess)
+            return -ENOMEM;
         c->mtu_chunks = chunks;
     }
     return 0;
@@ -398,8 +407,13 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     // flight (2048 lines: 16 KiB of LDS per table workgroup, ten per CU instead of five).
     uint64_t all_records = 0;
     for (size_t j = 0; j < count; ++j) all_records += batches[j].max_records;
-    const uint32_t ch = all_records <= (uint64_t)(nds ? nds : 1) * 32u * kMtuChunk ? (uint32_t)kMtuChunkSmall
-                                                                                  : (uint32_t)kMtuChunk;
+    static const int ch_env = [] {   // developer A/B: SR_MTU_CH=2048 / 4096 forces the chunk size
+        const char *e = getenv("SR_MTU_CH");
+        return e ? atoi(e) : 0;
+    }();
+    uint32_t ch = all_records <= (uint64_t)(nds ? nds : 1) * 32u * kMtuChunk ? (uint32_t)kMtuChunkSmall
+                                                                            : (uint32_t)kMtuChunk;
+    if (ch_env == kMtuChunkSmall || ch_env == kMtuChunk) ch = (uint32_t)ch_env;
     uint32_t tiles = 0, chunks = 0;
     for (size_t j = 0; j < count; ++j) {
         const sr_pack_batch &b = batches[j];
@@ -440,7 +454,8 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     L.chunk_pk = c->d_mtu_chunks + 3 * (size_t)chunks;
     L.table = c->d_mtu_table;
     L.nx = reinterpret_cast<uint8_t *>(c->d_mtu_table + (((size_t)c->mtu_chunks * kMtuX + 1) & ~(size_t)1));
-    L.gp = c->d_mtu_gp;
+    L.plen = reinterpret_cast<uint16_t *>(c->d_mtu_gp);
+    L.gp0 = c->d_mtu_gp + (size_t)c->mtu_chunks * kMtuChunk / 2;
 #ifdef SR_MTU_STAMPS   // developer timeline: 8 stamps per chunk, read back with sr_mtu_stamps
     static uint64_t *d_dbg = nullptr;
     static size_t dbg_cap = 0;
@@ -468,11 +483,27 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
         hipLaunchKernelGGL(mtu_table_kernel<kMtuChunk>, dim3(chunks), dim3(kMtuTableBlock), 0, c->stream, L);
     else
         hipLaunchKernelGGL(mtu_table_kernel<kMtuChunkSmall>, dim3(chunks), dim3(kMtuTableBlock), 0, c->stream, L);
-    hipLaunchKernelGGL(mtu_chain_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
-    if (ch == (uint32_t)kMtuChunk)
-        hipLaunchKernelGGL(mtu_emit_kernel<kMtuChunk>, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
-    else
-        hipLaunchKernelGGL(mtu_emit_kernel<kMtuChunkSmall>, dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
+    // the chain inside the emit kernel (one lane per shard) up to 64 shards, else mtu_chain
+    static const bool walk_env = [] {   // developer A/B: SR_MTU_WALK=0 keeps mtu_chain
+        const char *e = getenv("SR_MTU_WALK");
+        return !(e && e[0] == '0');
+    }();
+    // (a batch's fill_out read as some batch's fill_in would change under the walks: mtu_chain reads
+    // every fill_in before the shard's fill_out is written)
+    bool walk = walk_env && nds <= 64;
+    for (size_t a = 0; walk && a < count; ++a)
+        for (size_t b = 0; walk && b < count; ++b) {
+            const uint16_t *in = batches[b].d_fill_in, *out = batches[a].d_fill_out;
+            if (in && out && in < out + nds && out < in + nds) walk = false;
+        }
+    if (!walk) hipLaunchKernelGGL(mtu_chain_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
+    if (ch == (uint32_t)kMtuChunk) {
+        if (walk) hipLaunchKernelGGL((mtu_emit_kernel<kMtuChunk, true>), dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
+        else hipLaunchKernelGGL((mtu_emit_kernel<kMtuChunk, false>), dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
+    } else {
+        if (walk) hipLaunchKernelGGL((mtu_emit_kernel<kMtuChunkSmall, true>), dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
+        else hipLaunchKernelGGL((mtu_emit_kernel<kMtuChunkSmall, false>), dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
 
