@@ -44,11 +44,15 @@ namespace srk {
 constexpr int kMtuTile = SR_MTU_TILE;            // records per sort tile (one wave; 1024: 16 loads in flight
                                                  // per lane, count + scatter 2-3 % faster than 512)
 #ifndef SR_MTU_CHUNK
-#define SR_MTU_CHUNK 4096
+#define SR_MTU_CHUNK 4608
 #endif
-constexpr int kMtuChunk = SR_MTU_CHUNK;          // sorted lines per packing chunk (the larger size)
+// sorted lines per packing chunk (the larger size): the most whose table kernel still runs eight
+// workgroups per CU (18 KiB of prefix sums; 20 KiB of LDS per workgroup at most), so that a launch
+// of up to 2048 x 4608 lines has every chunk resident at once
+constexpr int kMtuChunk = SR_MTU_CHUNK;
 constexpr int kMtuChunkSmall = 2048;             // ... the smaller: more chunks in flight, a longer chain
-static_assert(kMtuChunk <= 8192 && kMtuChunk % kMtuChunkSmall == 0, "chunk entries hold line indices in 16 bits");
+static_assert(kMtuChunk <= 8192 && kMtuChunk % 256 == 0 && kMtuChunkSmall % 256 == 0,
+              "chunk entries hold line indices in 16 bits; whole rows of 256 threads");
 constexpr int kMtuBlock = 256;                   // threads of the emit kernel (and the prefix helper's default)
 #ifndef SR_MTU_TABLE_BLOCK
 #define SR_MTU_TABLE_BLOCK 256
@@ -456,12 +460,15 @@ __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuCh
 // prefix sums and the chunk's bytes.
 template <int CH>
 struct MtuTableSmem {
-    uint32_t P[CH];        // inclusive prefix of the chunk's line lengths, then the doubling words:
-                           // last packet start reached from here << 16 | packets closed on the way
+    union {
+        uint32_t P[CH];        // inclusive prefix of the chunk's line lengths, then the doubling words:
+                               // last packet start reached from here << 16 | packets closed on the way
+        uint64_t e[kMtuP0];    // at the end, per first line j: packets closed << 32 | last start << 16 | fill out
+    };
     uint32_t P0[kMtuP0];   // P[0 .. kMtuP0 - 1]
-    uint64_t e[kMtuP0];    // per first line j: packets closed << 32 | last start << 16 | fill out
     uint32_t wsum[16];     // the prefix scan's wave sums
 };
+static_assert(kMtuChunkSmall >= 2 * kMtuP0, "the entries fit over the doubling words");
 
 template <int CH, int NT = kMtuTableBlock>
 __global__ __launch_bounds__(NT, 8) void mtu_table_kernel(MtuLaunch L) {
@@ -563,10 +570,13 @@ __global__ __launch_bounds__(NT, 8) void mtu_table_kernel(MtuLaunch L) {
     // packet from the last start l, the packet length stored above for l (this workgroup's own
     // global writes, ordered before the barriers since)
     const uint32_t hi = min(cnt, (uint32_t)kMtuWindow);
+    uint64_t ev = 0;
     if (tid < hi) {
         const uint32_t v = sm.P[tid], l = v >> 16;
-        sm.e[tid] = ((uint64_t)(1u + (v & 0xFFFFu)) << 32) | ((uint64_t)l << 16) | gpl[l];
+        ev = ((uint64_t)(1u + (v & 0xFFFFu)) << 32) | ((uint64_t)l << 16) | gpl[l];
     }
+    __syncthreads();   // every read of the doubling words before the entries overwrite them
+    if (tid < hi) sm.e[tid] = ev;
     __syncthreads();
     // incoming fills x0 .. x0 + per - 1 per thread: the first line over the cap moves down with x
     constexpr uint32_t per = (kMtuX + NT - 1) / NT;

@@ -12,7 +12,7 @@ T="python -u -m pytest -x -q --timeout 120 --timeout-method thread"
 timeout -k 10 300 $T tests/test_gpu_mtu.py tests/test_gpu_router_core.py > gpurun_out/${tag}_tests.log 2>&1 \
   || { tail -40 gpurun_out/${tag}_tests.log; exit 1; }
 tail -1 gpurun_out/${tag}_tests.log
-for envs in SR_MTU_CH=2048 SR_MTU_CH=4096 SR_MTU_WALK=0; do
+for envs in SR_MTU_CH=2048 SR_MTU_CH=4608 SR_MTU_WALK=0; do
   env $envs timeout -k 10 300 $T tests/test_gpu_mtu.py tests/test_gpu_router_core.py > gpurun_out/${tag}_tests_$envs.log 2>&1 \
     || { tail -40 gpurun_out/${tag}_tests_$envs.log; exit 1; }
   echo "$envs: $(tail -1 gpurun_out/${tag}_tests_$envs.log)"
