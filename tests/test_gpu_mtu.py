@@ -214,6 +214,39 @@ def test_pack_packets_device_many(pkg, oracle, torch_stream):
         fill = got_fill
 
 
+def test_pack_packets_fill_in_place(pkg, oracle, torch_stream):
+    """sr_pack_packets with d_fill_out aliasing d_fill_in (allowed by sr_route.h): the pending bytes
+    are read before they are overwritten whichever chain path runs (mtu_emit's walk reads every
+    shard's fill_in from every chunk, so an aliased launch takes mtu_chain instead)."""
+    import torch
+
+    for n, lens in ((8, [64, 256]), (3, [6, 7, 13])):
+        s = pkg.gen_stream(1 << 19, lens, seed=900 + n, p_invalid=0.05)
+        cap = s.n_lines
+        mp = pkg.max_packets(1 << 19, n)
+        d_in = torch.from_numpy(s.data.copy()).cuda()
+        d_rec = torch.zeros(cap, dtype=torch.int64, device="cuda")
+        d_cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+        d_srt = torch.zeros(cap, dtype=torch.int64, device="cuda")
+        d_pk = torch.zeros(mp * 2, dtype=torch.int64, device="cuda")
+        d_counts = torch.zeros(3, dtype=torch.int64, device="cuda")
+        fill = [(97 * k + 5) % 1451 for k in range(n)]
+        d_fill = torch.tensor(np.array(fill, dtype=np.uint16).view(np.int16), device="cuda")
+        with pkg.Router(n, 1 << 19) as r:
+            r.set_stream(torch_stream.cuda_stream)
+            r.route_device_many([(d_in.data_ptr(), int(s.data.size), d_rec.data_ptr(), cap, None, d_cnt.data_ptr())])
+            r.pack_packets(d_rec.data_ptr(), d_cnt.data_ptr(), cap, d_fill.data_ptr(), 0, d_srt.data_ptr(),
+                           d_pk.data_ptr(), mp, d_counts.data_ptr(), d_fill.data_ptr())
+            torch.cuda.synchronize()
+        recs, _, cnt = oracle.route(s.data, n, None)
+        srt_o, pk_o, fill_o, nv = oracle.pack_packets(recs, n, fill)
+        np_, nv_g, nl = d_counts.cpu().tolist()
+        assert (np_, nv_g, nl) == (len(pk_o), nv, cnt)
+        pk = np.frombuffer(d_pk.cpu().numpy().tobytes(), dtype=pkg.PACKET_DTYPE)[:np_]
+        assert np.array_equal(pk.view(np.uint8), pk_o.view(np.uint8)), "packet descriptors differ"
+        assert d_fill.cpu().numpy().view(np.uint16).tolist() == fill_o.tolist()
+
+
 def test_route_pack_edges(pkg, oracle):
     """Exact-fit packets, carry-only flushes, empty and single-line batches."""
     n = 2
