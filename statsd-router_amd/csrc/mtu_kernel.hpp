@@ -108,6 +108,7 @@ struct MtuLaunch {
     uint16_t *plen;                    // [chunks][kMtuChunk] bytes of the packet a line starts (mtu_table -> mtu_emit)
     uint32_t *gp0;                     // [chunks][kMtuP0 + 1] the first prefix sums and the chunk's bytes
     uint64_t *dbg;                     // SR_MTU_STAMPS developer builds only: 8 timestamps per chunk
+    uint32_t xcd;                      // chunk kernels: every batch's chunks on one XCD (mtu_chunk_slot)
     MtuBatchArg b[kMtuMaxBatches];
 };
 static_assert(sizeof(MtuLaunch) < 3584, "kernel argument size");
@@ -172,6 +173,23 @@ __device__ __forceinline__ MtuParams mtu_view(const MtuLaunch &L, uint32_t bi) {
     p.counts = a.counts;
     p.fill_out = a.fill_out;
     return p;
+}
+
+// The chunk slot of a chunk-kernel workgroup. With L.xcd (eight batches or more), workgroup B runs on
+// XCD B % 8 (the dispatcher deals workgroups to the XCDs in turn) and takes the (B / 8)-th slot of
+// the batches b = B (mod 8): every chunk of a batch on one XCD, so that the tables, next() and packet
+// lengths the table kernel writes are read from that XCD's L2 by the emit kernel (whose chain walk
+// reads one table entry per hop). kMtuNone: past the slots.
+__device__ __forceinline__ uint32_t mtu_chunk_slot(const MtuLaunch &L, uint32_t B) {
+    if (!L.xcd) return B < L.chunks ? B : kMtuNone;
+    const uint32_t x = B & 7u, k = B >> 3;
+    uint32_t acc = 0;
+    for (uint32_t b = x; b < L.nb; b += 8) {
+        const uint32_t s0 = L.b[b].chunk0, s1 = b + 1 < L.nb ? L.b[b + 1].chunk0 : L.chunks;
+        if (k < acc + (s1 - s0)) return s0 + (k - acc);
+        acc += s1 - s0;
+    }
+    return kMtuNone;
 }
 
 // the batch owning global index g of a per-batch sequence starting at field `first` (nb <= 32)
@@ -477,14 +495,16 @@ __global__ __launch_bounds__(NT, 8) void mtu_table_kernel(MtuLaunch L) {
     static_assert(NT >= kMtuP0, "one thread per kept prefix sum");
     __shared__ MtuTableSmem<CH> sm;
     MtuChunk ck;
-    const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.chunk0; });
+    const uint32_t gs = mtu_chunk_slot(L, blockIdx.x);
+    if (gs == kMtuNone) return;
+    const uint32_t bi = mtu_batch_of(L, gs, [](const MtuBatchArg &a) { return a.chunk0; });
     const MtuParams p = mtu_view(L, bi);
-    const uint32_t c = blockIdx.x - L.b[bi].chunk0;
+    const uint32_t c = gs - L.b[bi].chunk0;
     if (!mtu_chunk_of(p, c, ck)) return;
     const uint32_t tid = threadIdx.x;
-    mtu_stamp(L, blockIdx.x, 0);
+    mtu_stamp(L, gs, 0);
     mtu_chunk_prefix<CH, NT>(p, ck, sm.P, sm.wsum);
-    mtu_stamp(L, blockIdx.x, 1);
+    mtu_stamp(L, gs, 1);
     const uint32_t cnt = ck.cnt, total = sm.P[cnt - 1];
     uint32_t *gp0 = p.gp0 + (size_t)c * (kMtuP0 + 1);
     if (tid < (uint32_t)kMtuP0) {
@@ -544,7 +564,7 @@ __global__ __launch_bounds__(NT, 8) void mtu_table_kernel(MtuLaunch L) {
         sm.P[i] = nxt == kMtuEnd ? i << 16 : (nxt << 16) | 1u;   // past the chunk: self loops
     }
     __syncthreads();
-    mtu_stamp(L, blockIdx.x, 2);
+    mtu_stamp(L, gs, 2);
     // pointer doubling: ld -> the last packet start of the chain and the packets closed on it. A
     // chain closes at most 2 * total / (cap + 1) + 1 packets (two consecutive closed packets exceed
     // the cap together), so that many jumps suffice. In place, one barrier per round: a neighbour
@@ -565,7 +585,7 @@ __global__ __launch_bounds__(NT, 8) void mtu_table_kernel(MtuLaunch L) {
         }
         __syncthreads();
     }
-    mtu_stamp(L, blockIdx.x, 3);
+    mtu_stamp(L, gs, 3);
     // one entry per possible first line j (< 242 <= kMtuP0): the fill out is the bytes of the open
     // packet from the last start l, the packet length stored above for l (this workgroup's own
     // global writes, ordered before the barriers since)
@@ -600,7 +620,7 @@ __global__ __launch_bounds__(NT, 8) void mtu_table_kernel(MtuLaunch L) {
         }
         row[x] = e;
     }
-    mtu_stamp(L, blockIdx.x, 4);
+    mtu_stamp(L, gs, 4);
 }
 
 // One workgroup: the chunks of every shard composed in order, descriptor slots scanned.
@@ -677,11 +697,13 @@ __global__ __launch_bounds__(kMtuBlock, 8) void mtu_emit_kernel(MtuLaunch L) {  
     constexpr int kMtuPer = CH / kMtuBlock;
     __shared__ MtuEmitSmem<CH> sm;
     MtuChunk ck;
-    const uint32_t bi = mtu_batch_of(L, blockIdx.x, [](const MtuBatchArg &a) { return a.chunk0; });
+    const uint32_t gs = mtu_chunk_slot(L, blockIdx.x);
+    if (gs == kMtuNone) return;
+    const uint32_t bi = mtu_batch_of(L, gs, [](const MtuBatchArg &a) { return a.chunk0; });
     const MtuParams p = mtu_view(L, bi);
-    const uint32_t c = blockIdx.x - L.b[bi].chunk0;
+    const uint32_t c = gs - L.b[bi].chunk0;
     if (!mtu_chunk_of(p, c, ck)) return;
-    mtu_stamp(L, blockIdx.x, 5);
+    mtu_stamp(L, gs, 5);
     const int tid = threadIdx.x;
     const uint32_t *gp0 = p.gp0 + (size_t)c * (kMtuP0 + 1);
     const uint16_t *gpl = p.plen + (size_t)c * kMtuChunk;
@@ -759,7 +781,7 @@ __global__ __launch_bounds__(kMtuBlock, 8) void mtu_emit_kernel(MtuLaunch L) {  
         if (v * 16 < (uint32_t)CH) reinterpret_cast<uint4 *>(sm.nx)[v] = nxv[k];
     }
     __syncthreads();
-    mtu_stamp(L, blockIdx.x, 6);
+    mtu_stamp(L, gs, 6);
     uint16_t jv[kMtuPer];
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) {
@@ -825,7 +847,7 @@ __global__ __launch_bounds__(kMtuBlock, 8) void mtu_emit_kernel(MtuLaunch L) {  
             s0 = bs[step];
         }
     }
-    mtu_stamp(L, blockIdx.x, 7);
+    mtu_stamp(L, gs, 7);
 }
 
 }  // namespace srk

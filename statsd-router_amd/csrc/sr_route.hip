@@ -471,6 +471,23 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
 #else
     L.dbg = nullptr;
 #endif
+    // the chunk kernels' grid: eight batches or more put each batch's chunks on one XCD
+    // (mtu_chunk_slot): eight times the most slots any XCD takes
+    static const bool xcd_env = [] {   // developer A/B: SR_MTU_XCD=0 deals the chunks in launch order
+        const char *e = getenv("SR_MTU_XCD");
+        return !(e && e[0] == '0');
+    }();
+    uint32_t chunk_grid = chunks;
+    L.xcd = (xcd_env && count >= 8) ? 1u : 0u;
+    if (L.xcd) {
+        uint32_t per[8] = {0, 0, 0, 0, 0, 0, 0, 0}, mx = 0;
+        for (size_t j = 0; j < count; ++j) {
+            const uint32_t s1 = j + 1 < count ? L.b[j + 1].chunk0 : chunks;
+            per[j & 7] += s1 - L.b[j].chunk0;
+        }
+        for (int x = 0; x < 8; ++x) mx = per[x] > mx ? per[x] : mx;
+        chunk_grid = 8 * mx;
+    }
     const size_t sort_lds = (size_t)kMtuSortWaves * (nds + 1) * sizeof(uint32_t);
     // up to 4 x 4097 counters: past the 64 KiB default
     ensure_dyn_lds((const void *)mtu_count_kernel, 96 * 1024);
@@ -480,9 +497,9 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     hipLaunchKernelGGL(mtu_scan_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
     hipLaunchKernelGGL(mtu_scatter_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
     if (ch == (uint32_t)kMtuChunk)
-        hipLaunchKernelGGL(mtu_table_kernel<kMtuChunk>, dim3(chunks), dim3(kMtuTableBlock), 0, c->stream, L);
+        hipLaunchKernelGGL(mtu_table_kernel<kMtuChunk>, dim3(chunk_grid), dim3(kMtuTableBlock), 0, c->stream, L);
     else
-        hipLaunchKernelGGL(mtu_table_kernel<kMtuChunkSmall>, dim3(chunks), dim3(kMtuTableBlock), 0, c->stream, L);
+        hipLaunchKernelGGL(mtu_table_kernel<kMtuChunkSmall>, dim3(chunk_grid), dim3(kMtuTableBlock), 0, c->stream, L);
     // the chain inside the emit kernel (one lane per shard) up to 64 shards, else mtu_chain
     static const bool walk_env = [] {   // developer A/B: SR_MTU_WALK=0 keeps mtu_chain
         const char *e = getenv("SR_MTU_WALK");
@@ -498,11 +515,11 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
         }
     if (!walk) hipLaunchKernelGGL(mtu_chain_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
     if (ch == (uint32_t)kMtuChunk) {
-        if (walk) hipLaunchKernelGGL((mtu_emit_kernel<kMtuChunk, true>), dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
-        else hipLaunchKernelGGL((mtu_emit_kernel<kMtuChunk, false>), dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
+        if (walk) hipLaunchKernelGGL((mtu_emit_kernel<kMtuChunk, true>), dim3(chunk_grid), dim3(kMtuBlock), 0, c->stream, L);
+        else hipLaunchKernelGGL((mtu_emit_kernel<kMtuChunk, false>), dim3(chunk_grid), dim3(kMtuBlock), 0, c->stream, L);
     } else {
-        if (walk) hipLaunchKernelGGL((mtu_emit_kernel<kMtuChunkSmall, true>), dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
-        else hipLaunchKernelGGL((mtu_emit_kernel<kMtuChunkSmall, false>), dim3(chunks), dim3(kMtuBlock), 0, c->stream, L);
+        if (walk) hipLaunchKernelGGL((mtu_emit_kernel<kMtuChunkSmall, true>), dim3(chunk_grid), dim3(kMtuBlock), 0, c->stream, L);
+        else hipLaunchKernelGGL((mtu_emit_kernel<kMtuChunkSmall, false>), dim3(chunk_grid), dim3(kMtuBlock), 0, c->stream, L);
     }
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
 }
