@@ -142,34 +142,6 @@ __device__ __forceinline__ void pin64(uint64_t &x) {
     x = ((uint64_t)hi << 32) | lo;
 }
 
-// find_downstream's first picks (sr-main.c:86-117; probe_shard's first loop): all alive, h % N;
-// one dead shard, at most two picks (the second pick never meets the dead shard); two or more
-// dead, RouteParams::picks picks and then kRouteDefer (probe_defer_kernel finishes the probe; the
-// host launches this kernel only when it can defer). Reciprocals and alive words from the LDS
-// pads, the dead shards visited noted in the tile's LDS words (MARK_LDS).
-__device__ __forceinline__ uint32_t chunk_probe(uint64_t h, const RouteParams &p, uint32_t *img) {
-    const uint32_t n = p.nds;
-    if (p.dead >= n) return SR_ROUTE_ALL_DEAD;   // includes N == 0 (:115-116)
-    if (p.dead == 0) return mod_magic(h, p.magic_n, n);
-    const bool small = n <= 64;
-    const uint64_t alive0 = small ? ((uint64_t)alive_pad_dword(img, 32) << 32) | alive_pad_dword(img, 0) : 0ull;
-    const int np = p.dead >= 2 && p.picks == 1 ? 1 : 2;
-    uint32_t o0 = 0xFFFFFFFFu;   // the permutation overlay after one pick: (position << 16) | value
-    uint32_t i = n;
-    for (int it = 0; it < np; ++it, --i) {
-        const uint32_t j = mod_magic(h, magic_from_pad(img, n - i), i);                  // :98
-        const uint32_t k = (o0 >> 16) == j ? (o0 & 0xFFFFu) : j;                         // :99
-        const bool al = small ? ((alive0 >> k) & 1ull) != 0
-                              : (n <= 64 * kAliveLds ? ((alive_pad_dword(img, k) >> (k & 31)) & 1u) != 0
-                                                     : alive_bit(p.alive, k));
-        if (al) return k;                                                                 // :101-104
-        if (p.mark) note_dead_lds(img, k);                                                // :106
-        if (j != i - 1) o0 = (j << 16) | (i - 1);                                         // :108-111
-        h = (h * 7 + 5) / 3;                                                              // :113
-    }
-    return kRouteDefer;
-}
-
 template <unsigned ABL>
 __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) void route_chunk_kernel(RouteParams p) {
     __shared__ ChunkSmem sm;

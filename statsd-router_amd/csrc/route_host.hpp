@@ -438,6 +438,12 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
             hipLaunchKernelGGL((route_kernel<BLOCK, KV_UNIFORM>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
         else
             hipLaunchKernelGGL((route_chunk_kernel<ABL>), dim3(p.total_blocks), dim3(256), 0, stream, p);
+    } else if constexpr ((ABL & KV_PICKS) != 0) {
+        // the picks-only variant needs the deferral once two or more shards are dead
+        if (ds.dead >= 2 && ds.dead < ds.nds && !p.defer)
+            hipLaunchKernelGGL((route_kernel<BLOCK, (ABL & ~KV_PICKS)>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
+        else
+            hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     } else {
         hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     }

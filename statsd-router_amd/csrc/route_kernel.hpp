@@ -95,7 +95,10 @@ enum : unsigned {
 // lengths out one lane per 64-byte name segment (route_host.hpp picks the variant per launch).
 // KV_ALIVE: a launch whose every shard is alive (the shard is h % N): no probe, overlay, deferral or
 // probed-dead marks in the kernel, and none of their registers.
-enum : unsigned { KV_UNIFORM = 0u, KV_SEGMENTS = 4194304u, KV_ALIVE = 268435456u };
+// KV_PICKS: a launch with dead shards whose probes end after the first picks (one dead shard: two
+// picks always find a live one; two or more: the deferral of probe_defer_kernel) runs a variant
+// with chunk_probe in place of probe_shard, whose 16-entry overlay loop it cannot reach.
+enum : unsigned { KV_UNIFORM = 0u, KV_SEGMENTS = 4194304u, KV_ALIVE = 268435456u, KV_PICKS = 536870912u };
 
 constexpr uint64_t ipow(uint64_t b, unsigned e) {
     uint64_t r = 1;
@@ -681,6 +684,34 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark
         h = (h * 7 + 5) / 3;                                         // :113
     }
     return SR_ROUTE_ALL_DEAD;                                        // :115-116
+}
+
+// find_downstream's first picks (sr-main.c:86-117; probe_shard's first loop): all alive, h % N;
+// one dead shard, at most two picks (the second pick never meets the dead shard); two or more
+// dead, RouteParams::picks picks and then kRouteDefer (probe_defer_kernel finishes the probe; the
+// host launches this kernel only when it can defer). Reciprocals and alive words from the LDS
+// pads, the dead shards visited noted in the tile's LDS words (MARK_LDS).
+__device__ __forceinline__ uint32_t chunk_probe(uint64_t h, const RouteParams &p, uint32_t *img) {
+    const uint32_t n = p.nds;
+    if (p.dead >= n) return SR_ROUTE_ALL_DEAD;   // includes N == 0 (:115-116)
+    if (p.dead == 0) return mod_magic(h, p.magic_n, n);
+    const bool small = n <= 64;
+    const uint64_t alive0 = small ? ((uint64_t)alive_pad_dword(img, 32) << 32) | alive_pad_dword(img, 0) : 0ull;
+    const int np = p.dead >= 2 && p.picks == 1 ? 1 : 2;
+    uint32_t o0 = 0xFFFFFFFFu;   // the permutation overlay after one pick: (position << 16) | value
+    uint32_t i = n;
+    for (int it = 0; it < np; ++it, --i) {
+        const uint32_t j = mod_magic(h, magic_from_pad(img, n - i), i);                  // :98
+        const uint32_t k = (o0 >> 16) == j ? (o0 & 0xFFFFu) : j;                         // :99
+        const bool al = small ? ((alive0 >> k) & 1ull) != 0
+                              : (n <= 64 * kAliveLds ? ((alive_pad_dword(img, k) >> (k & 31)) & 1u) != 0
+                                                     : alive_bit(p.alive, k));
+        if (al) return k;                                                                 // :101-104
+        if (p.mark) note_dead_lds(img, k);                                                // :106
+        if (j != i - 1) o0 = (j << 16) | (i - 1);                                         // :108-111
+        h = (h * 7 + 5) / 3;                                                              // :113
+    }
+    return kRouteDefer;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1509,6 +1540,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
                 else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
                 else if (ABL & KV_ALIVE) route = p.nds ? mod_magic(h, p.magic_n, p.nds) : SR_ROUTE_ALL_DEAD;   // :145
+                else if (ABL & KV_PICKS) route = chunk_probe(h, p, sm.img);                          // :145
                 else route = probe_shard(h, p, nullptr, sm.img, nullptr, p.defer != 0,
                                          p.mark ? sm.img : nullptr);                                // :145
                 // a probe past its first two picks goes to probe_defer_kernel: the record is marked

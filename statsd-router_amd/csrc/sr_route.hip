@@ -88,8 +88,8 @@ static int launch_product(DeviceState &ds, const RouteParams &p, hipStream_t str
         if (seg) return launch_route<kBlock, KV_SEGMENTS | KV_ALIVE>(ds, p, stream);
         return launch_route<kBlock, KV_UNIFORM | KV_ALIVE>(ds, p, stream);
     }
-    if (seg) return launch_route<kBlock, KV_SEGMENTS>(ds, p, stream);
-    return launch_route<kBlock, KV_UNIFORM>(ds, p, stream);
+    if (seg) return launch_route<kBlock, KV_SEGMENTS | KV_PICKS>(ds, p, stream);
+    return launch_route<kBlock, KV_UNIFORM | KV_PICKS>(ds, p, stream);
 }
 #ifdef SR_ABLATION_VARIANTS
 static int launch_variant(DeviceState &ds, const RouteParams &p, hipStream_t stream) {

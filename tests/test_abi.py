@@ -118,8 +118,9 @@ def test_generator_is_deterministic_and_framed(pkg, oracle):
 def test_product_library_has_only_the_product_route_kernels(pkg):
     """Ablation variants (some write wrong records by design) never ship: the product library holds
     exactly the three lane layouts, KV_UNIFORM (0), KV_SEGMENTS (4194304) and KV_CHUNKS (8388608,
-    route_chunk_kernel), each also as KV_ALIVE (+268435456: launches with every shard alive),
-    which write identical records (tests/test_gpu_layout.py); ablations live in tools/ and
+    route_chunk_kernel), each also as KV_ALIVE (+268435456: launches with every shard alive), the
+    first two also as KV_PICKS (+536870912: probes that end after their first picks), which write
+    identical records (tests/test_gpu_layout.py); ablations live in tools/ and
     `make VARIANTS=1` builds only."""
     out = subprocess.run(["nm", "-C", pkg.ROUTE_LIB], capture_output=True, text=True).stdout
     kernels = {l.split(" ", 2)[-1] for l in out.splitlines()
@@ -128,6 +129,8 @@ def test_product_library_has_only_the_product_route_kernels(pkg):
                        "void srk::route_kernel<256, 4194304u>(srk::RouteParams)",
                        "void srk::route_kernel<256, 268435456u>(srk::RouteParams)",     # KV_ALIVE
                        "void srk::route_kernel<256, 272629760u>(srk::RouteParams)",     # KV_SEGMENTS | KV_ALIVE
+                       "void srk::route_kernel<256, 536870912u>(srk::RouteParams)",     # KV_PICKS
+                       "void srk::route_kernel<256, 541065216u>(srk::RouteParams)",     # KV_SEGMENTS | KV_PICKS
                        "void srk::route_chunk_kernel<8388608u>(srk::RouteParams)",
                        "void srk::route_chunk_kernel<276824064u>(srk::RouteParams)"}, kernels   # | KV_ALIVE
     assert b"SR_VARIANT" not in open(pkg.ROUTE_LIB, "rb").read()
