@@ -689,8 +689,9 @@ __device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark
 // find_downstream's first picks (sr-main.c:86-117; probe_shard's first loop): all alive, h % N;
 // one dead shard, at most two picks (the second pick never meets the dead shard); two or more
 // dead, RouteParams::picks picks and then kRouteDefer (probe_defer_kernel finishes the probe; the
-// host launches this kernel only when it can defer). Reciprocals and alive words from the LDS
-// pads, the dead shards visited noted in the tile's LDS words (MARK_LDS).
+// host launches a kernel using it only when it can defer). Reciprocals and alive words from the LDS
+// pads, the dead shards visited noted in the tile's LDS words (MARK_LDS). The probe of the chunk
+// kernel and of the route kernel's KV_PICKS variants.
 __device__ __forceinline__ uint32_t chunk_probe(uint64_t h, const RouteParams &p, uint32_t *img) {
     const uint32_t n = p.nds;
     if (p.dead >= n) return SR_ROUTE_ALL_DEAD;   // includes N == 0 (:115-116)
