@@ -435,10 +435,11 @@ __device__ __forceinline__ uint32_t mtu_first_over(const uint32_t *P, uint32_t l
 // running sum carried across the wave's 16 rows by DPP scans; one barrier for the wave offsets.
 template <int CH, int NT = kMtuBlock>
 __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuChunk &ck, uint32_t *P,
-                                                 uint32_t *wsum) {
-    constexpr int kMtuPer = CH / NT;
+                                                 uint32_t *wsum, uint32_t &lmin, uint32_t &lmax) {
+    constexpr int kMtuPer = CH / NT, kWaves = NT / 64;
     if (SR_MTU_SKIP & 16) {
         for (uint32_t i = threadIdx.x; i < (uint32_t)CH; i += NT) P[i] = 64u * (i + 1);
+        lmin = lmax = 64u;
         __syncthreads();
         return;
     }
@@ -451,16 +452,35 @@ __device__ __forceinline__ void mtu_chunk_prefix(const MtuParams &p, const MtuCh
         const uint32_t len = p.sorted[ck.pos0 + min(i, ck.cnt - 1)].length;
         v[k] = i < ck.cnt ? len : 0u;
     }
+    uint32_t mn = 0xFFFFFFFFu, mx = 0;   // the chunk's shortest and longest line (bounds next())
+#pragma unroll
+    for (int k = 0; k < kMtuPer; ++k) {
+        const bool in = base + 64u * k < ck.cnt;
+        mn = min(mn, in ? v[k] : 0xFFFFFFFFu);
+        mx = max(mx, v[k]);
+    }
+    mn = wave_incl_min32(mn);
+    mx = wave_incl_max32(mx);
     uint32_t carry = 0;
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) {
         v[k] = wave_incl_add32(v[k]) + carry;
         carry = (uint32_t)__builtin_amdgcn_readlane((int)v[k], 63);
     }
-    if (lane == 63) wsum[wave] = carry;
+    if (lane == 63) {
+        wsum[wave] = carry;
+        wsum[kWaves + wave] = mn;
+        wsum[2 * kWaves + wave] = mx;
+    }
     __syncthreads();
     uint32_t add = 0;
     for (int w = 0; w < wave; ++w) add += wsum[w];
+    lmin = wsum[kWaves];
+    lmax = wsum[2 * kWaves];
+    for (int w = 1; w < kWaves; ++w) {
+        lmin = min(lmin, wsum[kWaves + w]);
+        lmax = max(lmax, wsum[2 * kWaves + w]);
+    }
 #pragma unroll
     for (int k = 0; k < kMtuPer; ++k) P[base + 64u * k] = v[k] + add;
     __syncthreads();
@@ -484,7 +504,7 @@ struct MtuTableSmem {
         uint64_t e[kMtuP0];    // at the end, per first line j: packets closed << 32 | last start << 16 | fill out
     };
     uint32_t P0[kMtuP0];   // P[0 .. kMtuP0 - 1]
-    uint32_t wsum[16];     // the prefix scan's wave sums
+    uint32_t wsum[48];     // the prefix scan's wave sums, then the waves' shortest and longest lines
 };
 static_assert(kMtuChunkSmall >= 2 * kMtuP0, "the entries fit over the doubling words");
 
@@ -503,7 +523,8 @@ __global__ __launch_bounds__(NT, 8) void mtu_table_kernel(MtuLaunch L) {
     if (!mtu_chunk_of(p, c, ck)) return;
     const uint32_t tid = threadIdx.x;
     mtu_stamp(L, gs, 0);
-    mtu_chunk_prefix<CH, NT>(p, ck, sm.P, sm.wsum);
+    uint32_t lmin, lmax;
+    mtu_chunk_prefix<CH, NT>(p, ck, sm.P, sm.wsum, lmin, lmax);
     mtu_stamp(L, gs, 1);
     const uint32_t cnt = ck.cnt, total = sm.P[cnt - 1];
     uint32_t *gp0 = p.gp0 + (size_t)c * (kMtuP0 + 1);
@@ -519,6 +540,14 @@ __global__ __launch_bounds__(NT, 8) void mtu_table_kernel(MtuLaunch L) {
     // fewer than 242). Every LDS read is unconditional at a clamped index (a read under a per-lane
     // condition becomes a branch with its own wait); past the chunk the clamped read gives
     // P[cnt - 1] = total. kHalf rows at a time (registers), results packed two per register.
+    // The chunk's line lengths bound the search (workgroup-uniform): a packet from i holds at least
+    // cap / lmax lines and at most cap / lmin (a line over the cap is a packet alone), so lo lies in
+    // [i + lo_a, i + lo_b], inside the span searched from i + lo_a; with one line length (C2-C4)
+    // the span is 1 and no step runs.
+    const uint32_t lo_a = lmax && lmax <= (uint32_t)kMtuCap ? (uint32_t)kMtuCap / lmax - 1u : 0u;
+    const uint32_t lo_b = !lmin ? 255u : lmin <= (uint32_t)kMtuCap ? (uint32_t)kMtuCap / lmin - 1u : 0u;
+    const uint32_t d = lo_b - lo_a;   // the smallest power of two span > d
+    const uint32_t span = d >= 128u ? 256u : d ? 2u << (31 - __builtin_clz(d)) : 1u;
     uint32_t nxp[(kMtuPer + 1) / 2];
     uint8_t *gnx = p.nx + (size_t)c * kMtuChunk;
     uint16_t *gpl = p.plen + (size_t)c * kMtuChunk;
@@ -528,12 +557,12 @@ __global__ __launch_bounds__(NT, 8) void mtu_table_kernel(MtuLaunch L) {
 #pragma unroll
         for (int k = 0; k < kHalf; ++k) {
             const uint32_t i = tid + (uint32_t)(h + k) * NT;
-            lo[k] = i;   // P[i] <= lim: a line alone always fits
+            lo[k] = i + lo_a;   // P[i + lo_a] <= lim (or the chunk ends first: see end)
             const uint32_t pm = sm.P[min(i ? i - 1 : 0u, cnt - 1)];
             lim[k] = pm * (uint32_t)(i != 0) + (uint32_t)kMtuCap;
         }
 #pragma unroll
-        for (uint32_t step = 128; step; step >>= 1) {
+        for (uint32_t step = span >> 1; step; step >>= 1) {
 #pragma unroll
             for (int k = 0; k < kHalf; ++k) {
                 const uint32_t t = lo[k] + step;

@@ -35,6 +35,11 @@ STREAMS = [
     ([64], 4, 1.0, 0.0, 1 << 16, 11),              # every downstream dead
     ([6, 7], 1, 0.0, 0.0, 1 << 20, 12),            # one shard, > 131 k line capacity: 4096-line chunks
     ([6, 7], 2, 0.5, 0.0, 1 << 20, 13),            # the same through the probe, one shard alive
+    # narrow length ranges: the table kernel's next() search runs only over [cap / max, cap / min]
+    ([145, 146], 3, 0.0, 0.0, 1 << 19, 14),        # 9 or 10 lines a packet: a 2-wide search
+    ([483, 484, 725, 726], 4, 0.0, 0.0, 1 << 19, 15),
+    ([1449], 2, 0.0, 0.0, 1 << 18, 16),            # one line a packet: no search
+    ([725], 3, 0.0, 0.1, 1 << 18, 17),             # exactly two lines a packet
 ]
 
 
