@@ -561,8 +561,7 @@ __global__ __launch_bounds__(NT, 8) void mtu_table_kernel(MtuLaunch L) {
             const uint32_t pm = sm.P[min(i ? i - 1 : 0u, cnt - 1)];
             lim[k] = pm * (uint32_t)(i != 0) + (uint32_t)kMtuCap;
         }
-#pragma unroll
-        for (uint32_t step = span >> 1; step; step >>= 1) {
+        for (uint32_t step = span >> 1; step; step >>= 1) {   // 0-8 steps, a workgroup-uniform loop
 #pragma unroll
             for (int k = 0; k < kHalf; ++k) {
                 const uint32_t t = lo[k] + step;
