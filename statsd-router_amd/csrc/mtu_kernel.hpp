@@ -64,6 +64,10 @@ constexpr int kMtuWindow = kMtuCap / (int)SR_MIN_LINE_LENGTH + 1;   // a packet 
 constexpr int kMtuX = kMtuCap + 1;               // incoming fills 0..1450
 constexpr uint32_t kMtuNone = 0xFFFFFFFFu;
 constexpr uint16_t kMtuEnd = 0xFFFFu;
+#ifndef SR_MTU_TAIL_HOPS
+#define SR_MTU_TAIL_HOPS 16
+#endif
+constexpr int kMtuTailHops = SR_MTU_TAIL_HOPS;   // mtu_table: jumps each entry walks after the doubling
 constexpr int kMtuP0 = 256;                      // prefix sums kept per chunk for the first line over the cap
 static_assert(kMtuWindow <= kMtuP0, "the incoming packet closes within a chunk's first kMtuP0 lines");
 
@@ -595,11 +599,14 @@ __global__ __launch_bounds__(NT, 8) void mtu_table_kernel(MtuLaunch L) {
     mtu_stamp(L, gs, 2);
     // pointer doubling: ld -> the last packet start of the chain and the packets closed on it. A
     // chain closes at most 2 * total / (cap + 1) + 1 packets (two consecutive closed packets exceed
-    // the cap together), so that many jumps suffice. In place, one barrier per round: a neighbour
-    // read mid-round has jumped at least as far as at the round's start, so after r rounds every
-    // jump spans >= 2^r starts (or ends the chain).
-    const uint32_t kb = min(cnt, 2u * total / (uint32_t)(kMtuCap + 1) + 2u);
-    for (uint32_t span = 1; span < kb; span <<= 1) {
+    // the cap together), and at most cnt / (lo_a + 1) (a closed packet holds lo_a + 1 lines or more),
+    // so that many jumps suffice. In place, one barrier per round: a neighbour read mid-round has
+    // jumped at least as far as at the round's start, so after r rounds every jump spans >= 2^r
+    // starts (or ends the chain). Only the first hi lines' chains are read, so the rounds stop once
+    // kMtuTailHops jumps finish every chain, and those lines walk the rest (each word is a valid
+    // jump: (start reached << 16) | packets closed, 0 closed = the chain's last start).
+    const uint32_t kb = min(min(cnt, 2u * total / (uint32_t)(kMtuCap + 1) + 2u), cnt / (lo_a + 1u) + 2u);
+    for (uint32_t span = 1; span * (uint32_t)kMtuTailHops < kb; span <<= 1) {
 #pragma unroll
         for (int h = 0; h < kMtuPer; h += kHalf) {
             uint32_t v[kHalf], w[kHalf];
@@ -620,8 +627,13 @@ __global__ __launch_bounds__(NT, 8) void mtu_table_kernel(MtuLaunch L) {
     const uint32_t hi = min(cnt, (uint32_t)kMtuWindow);
     uint64_t ev = 0;
     if (tid < hi) {
-        const uint32_t v = sm.P[tid], l = v >> 16;
-        ev = ((uint64_t)(1u + (v & 0xFFFFu)) << 32) | ((uint64_t)l << 16) | gpl[l];
+        const uint32_t v = sm.P[tid];
+        uint32_t l = v >> 16, closed = v & 0xFFFFu;
+        for (uint32_t w = sm.P[l]; w & 0xFFFFu; w = sm.P[l]) {   // at most kMtuTailHops jumps
+            closed += w & 0xFFFFu;
+            l = w >> 16;
+        }
+        ev = ((uint64_t)(1u + closed) << 32) | ((uint64_t)l << 16) | gpl[l];
     }
     __syncthreads();   // every read of the doubling words before the entries overwrite them
     if (tid < hi) sm.e[tid] = ev;
