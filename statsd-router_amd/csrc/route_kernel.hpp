@@ -702,7 +702,10 @@ __device__ __forceinline__ uint32_t chunk_probe(uint64_t h, const RouteParams &p
     uint32_t o0 = 0xFFFFFFFFu;   // the permutation overlay after one pick: (position << 16) | value
     uint32_t i = n;
     for (int it = 0; it < np; ++it, --i) {
-        const uint32_t j = mod_magic(h, magic_from_pad(img, n - i), i);                  // :98
+        // the first pick's reciprocal is the kernel argument (scalar registers, a scalar branch on
+        // its kind), the second's an LDS pad
+        const Magic mg = it == 0 ? p.magic_n : magic_from_pad(img, n - i);
+        const uint32_t j = mod_magic(h, mg, i);                                           // :98
         const uint32_t k = (o0 >> 16) == j ? (o0 & 0xFFFFu) : j;                         // :99
         const bool al = small ? ((alive0 >> k) & 1ull) != 0
                               : (n <= 64 * kAliveLds ? ((alive_pad_dword(img, k) >> (k & 31)) & 1u) != 0
