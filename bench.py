@@ -91,6 +91,9 @@ def parse(argv=None):
                          "route launches overlap: a rocprof mean over the run then mixes in stretched launches)")
     ap.add_argument("--layout", default="auto", choices=["auto", "uniform", "segments", "chunks"],
                     help="route kernel lane layout (sr_set_layout; records identical either way)")
+    ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
+                    help="sr_set_knob on the bench's contexts (A/B runs): lb_spin, defer_picks, mtu_chunk, mtu_xcd, "
+                         "mtu_walk (results never change)")
     ap.add_argument("--dry-ranks", action="store_true",
                     help="each rank prints its RANK / LOCAL_RANK / WORLD_SIZE and exits (launcher test; no GPU)")
     # the PMC counter bytes of the dominant kernel (tools/pmc_summary.py): at the top of the tree so
@@ -199,6 +202,7 @@ def main(argv=None):
     router = pkg.Router(shards, batch_bytes, device=local)
     router.set_alive(alive)
     router.set_stream(stream.cuda_stream)
+    apply_knobs(pkg, router, args.knob)
     router.set_layout({"auto": pkg.SR_LAYOUT_AUTO, "uniform": pkg.SR_LAYOUT_UNIFORM,
                        "segments": pkg.SR_LAYOUT_SEGMENTS, "chunks": pkg.SR_LAYOUT_CHUNKS}[args.layout])
     in_ptr, out_ptr, cnt_ptr = d_in.data_ptr(), d_out.data_ptr(), d_cnt.data_ptr()
@@ -279,7 +283,7 @@ def main(argv=None):
             # measured on this very build of the library and configuration
             lib_sha = hashlib.sha256(open(pkg.ROUTE_LIB, "rb").read()).hexdigest()
             if (tr.get("config") == args.config and tr.get("lib_sha256") == lib_sha
-                    and tr.get("kernel", kernel_name) == kernel_name):
+                    and tr.get("kernel") == kernel_name):   # the kernel named explicitly, no default
                 traffic = tr.get("hbm_bytes_per_launch")
                 traffic_src = f"{os.path.relpath(tj, REPO)} (rocprofv3 --pmc of this build, lib sha256 {lib_sha[:12]})"
             else:
@@ -301,7 +305,7 @@ def main(argv=None):
             "data": f"synthetic: seeded sr_gen streams, {B} distinct framed 16 MiB batches per GPU resident in HBM",
             "config": {
                 "workload": desc,
-                "step": f"one route_kernel launch over {M} distinct batches ({group_bytes[0]} B at group 0)",
+                "step": f"one {kernel_name} launch over {M} distinct batches ({group_bytes[0]} B at group 0)",
                 "batch_bytes": batch_bytes,
                 "line_bytes": lens,
                 "p_invalid": p_inv,
@@ -341,7 +345,10 @@ def main(argv=None):
             result["e2e"] = e2e(pkg, router, stream, host, sizes, lines, batch_bytes, dev, M)
         if not args.no_pack:
             result["route_pack"] = pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev,
-                                            dead=sum(alive) < shards, alive=alive, threads=args.pack_threads)
+                                            dead=sum(alive) < shards, alive=alive, threads=args.pack_threads,
+                                            host=None if args.no_verify else host, knobs=args.knob)
+        if args.knob:
+            result["config"]["knobs"] = args.knob
     router.close()
     del d_in, d_out
     torch.cuda.empty_cache()
@@ -382,6 +389,13 @@ def main(argv=None):
         dist.destroy_process_group()
     if dog is not None:
         dog.cancel()
+
+
+def apply_knobs(pkg, router, knobs):
+    """--knob NAME=VALUE: sr_set_knob (SR_KNOB_<NAME>) on a context."""
+    for kv in knobs:
+        name, _, val = kv.partition("=")
+        router.set_knob(getattr(pkg, "SR_KNOB_" + name.upper()), int(val, 0))
 
 
 def read_ceiling(d_in, stream, reps=20):
@@ -605,8 +619,40 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8, exchange="
                      f"trip per step for the split sizes")}
 
 
+def verify_pack(pkg, th, host, M, max_lines, shards, alive):
+    """After the route_pack leg's timing: replay its graph once more, then batch M - 1 of the launch
+    (sorted records, packet descriptors, counts, pending bytes out, probed-dead bitmap) against the
+    C oracle's push_to_downstream restatement. Raises on any difference."""
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import sr_oracle
+
+    with torch.cuda.stream(th.st):
+        th.g_all.replay()
+    th.st.synchronize()
+    m = M - 1
+    s = host[th.first + m]
+    recs, _, cn = sr_oracle.route(s.data, shards, alive)
+    probed = sr_oracle.probed_dead(s.data, shards, alive)
+    fill_in = th.fill[m].cpu().numpy().view(np.uint16)
+    srt_o, pk_o, fo_o, nv_o = sr_oracle.pack_packets(recs, shards, fill_in, probed)
+    np_, nv, nl = (int(x) for x in th.counts[m].cpu().tolist())
+    srt = np.frombuffer(th.srt[m].cpu().numpy().tobytes(), dtype=pkg.RECORD_DTYPE)[:nl]
+    pk = np.frombuffer(th.pk[m].cpu().numpy().tobytes(), dtype=pkg.PACKET_DTYPE)[:np_]
+    fo = th.fout[m].cpu().numpy().view(np.uint16)
+    pd = pkg.bitmap_shards(np.frombuffer(th.pd[m].cpu().numpy().tobytes(), dtype=np.uint64), shards)
+    if ((np_, nv, nl) != (len(pk_o), nv_o, cn) or not np.array_equal(srt, srt_o)
+            or not np.array_equal(pk.view(np.uint8), pk_o.view(np.uint8)) or fo.tolist() != fo_o.tolist()
+            or pd.tolist() != probed.tolist()):
+        raise SystemExit(f"route_pack leg: batch {m} of the timed graph differs from the oracle")
+    return (f"batch {m} of the timed route + pack graph ({cn} lines, {np_} packets) equals the C oracle: sorted "
+            "records, descriptors, counts, pending bytes out, probed-dead bitmap")
+
+
 def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev, dead=False, reps=20,
-             alive=None, threads=2):
+             alive=None, threads=2, host=None, knobs=()):
     """The router's device data path: one route launch over M batches (the
     batches of M data threads), then the per-downstream MTU packing of all of them in one
     sr_pack_packets_many (sorted records + packet descriptors, each batch from its own pending
@@ -688,6 +734,7 @@ def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, de
     t1 = Thread(router, stream, 0)
     t1.capture()
     res = {"route_pack": timed([t1], "g_all"), "route_only": timed([t1], "g_route")}
+    verify = None if host is None else verify_pack(pkg, t1, host, M, max_lines, shards, alive)
     packets = int(t1.counts[:, 0].sum())
     tot_lines = sum(lines[:M])
     out = {"value": round(tot_lines / (res["route_pack"] * 1e-3) / 1e6, 3), "unit": "M metrics/s",
@@ -695,6 +742,7 @@ def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, de
            "packing_ms": round(res["route_pack"] - res["route_only"], 4),
            "packets_per_launch": packets,
            "probed_dead_shards": int(sum(bin(int(w) & (2**64 - 1)).count("1") for w in t1.pd[0].tolist())),
+           "verify": verify,
            "note": (f"one route launch over {M} batches with their probed-dead bitmaps (sr-main.c:106) + one "
                     f"sr_pack_packets_many over them (regroup by downstream, next-fit 1450-byte packets), one "
                     f"graph, {reps} replays")}
@@ -704,6 +752,7 @@ def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, de
     r2 = pkg.Router(shards, batch_bytes, device=dev.index)
     try:
         r2.set_alive(alive if alive is not None else [1] * shards)
+        apply_knobs(pkg, r2, knobs)
         s2 = torch.cuda.Stream(device=dev)
         r2.set_stream(s2.cuda_stream)
         t2 = Thread(r2, s2, M if nsets > 1 else 0)

@@ -9,7 +9,8 @@
  *   - the flush of a packet: counters, then the bytes to the emit callback (ds_schedule_flush,
  *     sr-main.c:49-71; the send itself, ds_flush_cb :21-46, is the caller's);
  *   - the drop of a probed dead downstream's pending buffer (find_downstream, sr-main.c:106);
- *   - the WARN lines with the reference's texts (sr-main.c:115,142,184);
+ *   - the WARN lines with the reference's texts (sr-main.c:115,142,184) and, at log_level 0, the
+ *     TRACE lines (sr-main.c:91,102,174) in input order, from the GPU's per-line hashes;
  *   - the flush timer (ds_flush_timer_cb, :194-204) and the self-metrics (ping_cb, :206-235), whose
  *     few lines are routed on the GPU too and appended here with push_to_downstream's rule (:73-83).
  * There is no CPU routing path: the shard of every line, data or ping, comes from the GPU.
@@ -47,9 +48,14 @@ struct sr_core {
     size_t max_batch;
     uint8_t *in[2];                          /* the two slots' framed datagrams                 */
     const uint8_t *in_flight_bytes;          /* the framed bytes of the batch in flight          */
+    size_t in_flight_len;
     int in_flight;                           /* slot whose batch is on the GPU, or -1            */
-    unsigned fail_submit, submits;           /* fault injection (SR_CORE_FAIL_SUBMIT=k, tests):  */
-                                             /* the k-th sr_core_submit fails as a GPU error     */
+    unsigned fail_submit, submits;           /* fault injection (sr_core_inject_faults, tests)   */
+    unsigned fail_finish, finishes;
+    int trace;                               /* log_level TRACE: per-line hashes from the GPU     */
+    uint32_t *dg_ends[2];                    /* TRACE: datagram ends of the batch in each slot    */
+    size_t dg_n[2], dg_cap[2];
+    uint64_t *ping_hash;                     /* TRACE: the ping names' hashes                      */
     int host_fills;                          /* the host changed pending buffers since the last  */
                                              /* submission: upload them with the next one         */
     uint16_t *fill16;
@@ -129,6 +135,9 @@ void sr_core_close(sr_core *c) {
     free(c->iov);
     free(c->msg);
     free(c->ping);
+    free(c->ping_hash);
+    free(c->dg_ends[0]);
+    free(c->dg_ends[1]);
     free(c->alive);
     free(c->ds);
     free(c);
@@ -156,8 +165,13 @@ int sr_core_open(sr_core **out, const sr_core_config *cfg, sr_core_emit_fn emit,
         return rc;
     }
     c->in_flight = -1;
-    if (getenv("SR_CORE_FAIL_SUBMIT")) c->fail_submit = (unsigned)strtoul(getenv("SR_CORE_FAIL_SUBMIT"), NULL, 0);
     c->host_fills = 1;
+    /* TRACE (sr-init.c:252 default): every line's hash from the route kernel, records in input order */
+    c->trace = c->log_level <= SR_TRACE && c->log != NULL;
+    if (c->trace && (rc = sr_set_trace(c->ctx, 1))) {
+        sr_core_close(c);
+        return rc;
+    }
     c->msg_cap = 3 * SR_DATA_BUF_SIZE;
     c->ds = calloc(c->n, sizeof(ds_state));
     c->alive = calloc(c->nwords, sizeof(uint64_t));
@@ -171,8 +185,9 @@ int sr_core_open(sr_core **out, const sr_core_config *cfg, sr_core_emit_fn emit,
     c->in[0] = sr_alloc_host(cfg->max_batch_bytes);
     c->in[1] = sr_alloc_host(cfg->max_batch_bytes);
     c->sorted = sr_alloc_host(c->sorted_cap * sizeof(sr_record));
+    c->ping_hash = calloc(c->sorted_cap, sizeof(uint64_t));
     if (!c->ds || !c->alive || !c->fill16 || !c->probed || !c->iov || !c->msg || !c->ping || !c->in[0] ||
-        !c->in[1] || !c->sorted) {
+        !c->in[1] || !c->sorted || !c->ping_hash) {
         sr_core_close(c);
         return -ENOMEM;
     }
@@ -232,12 +247,50 @@ static void warn_line(sr_core *c, const uint8_t *framed, const sr_record *r) {
     }
 }
 
+/* find_downstream's TRACE lines for a line that passed the length and ':' tests (sr-main.c:91,102):
+ * its hash, then its first live pick, or the WARN when every downstream is dead (:115). */
+static void trace_line(sr_core *c, const char *line, int len, uint64_t h, uint32_t route) {
+    core_log(c, SR_TRACE, "%s: hash = %lx, length = %d, line = %.*s", "find_downstream", (unsigned long)h, len, len,
+             line);
+    if (route < c->n) core_log(c, SR_TRACE, "%s: pushing to downstream %d", "find_downstream", (int)route);
+    else core_log(c, SR_WARN, "%s: all downstreams are dead", "find_downstream");
+}
+
+/* TRACE: every message of udp_read_cb for the batch in slot `slot`, in input order: per datagram
+ * "got packet" (sr-main.c:174), then per line its WARN (:142,184) or its find_downstream lines. */
+static void trace_batch(sr_core *c, int slot, const uint8_t *framed, size_t nbytes) {
+    const sr_record *rec;
+    const uint64_t *hs;
+    size_t n = 0, i = 0, d0 = 0;
+    int rc = sr_route_pack_trace(c->ctx, slot, &rec, &hs, &n);
+    if (rc) {
+        core_log(c, SR_ERROR, "%s: sr_route_pack_trace() failed %s", "udp_read_cb", strerror(-rc));
+        return;
+    }
+    const size_t nd = c->dg_n[slot];
+    for (size_t g = 0; g <= nd; g++) {   /* the datagrams, then whatever no boundary covers */
+        const size_t end = g < nd ? c->dg_ends[slot][g] : nbytes;
+        if (g < nd)
+            core_log(c, SR_TRACE, "%s: got packet %.*s", "udp_read_cb", (int)(end - d0), (const char *)framed + d0);
+        for (; i < n && (g == nd || rec[i].offset < end); i++) {
+            if (rec[i].route == SR_ROUTE_INVALID_LENGTH || rec[i].route == SR_ROUTE_INVALID_FORMAT)
+                warn_line(c, framed, &rec[i]);
+            else
+                trace_line(c, (const char *)framed + rec[i].offset, rec[i].length, hs[i], rec[i].route);
+        }
+        d0 = end;
+    }
+    c->dg_n[slot] = 0;
+}
+
 /* The host's half of a batch (udp_read_cb's per-line side effects, sr-main.c:175-189, for a whole
- * batch): drop probed dead buffers, WARN lines in input order, then the packets per downstream. */
-static void complete(sr_core *c, const uint8_t *framed, const sr_pack_result *r) {
+ * batch): drop probed dead buffers, the log lines in input order, then the packets per downstream. */
+static void complete(sr_core *c, int slot, const uint8_t *framed, size_t nbytes, const sr_pack_result *r) {
     memcpy(c->probed, r->probed_dead, c->nwords * sizeof(uint64_t));
     drop_probed(c);
-    if (c->log_level <= SR_WARN)
+    if (c->trace)
+        trace_batch(c, slot, framed, nbytes);
+    else if (c->log_level <= SR_WARN)
         for (size_t i = r->n_valid; i < r->n_records; i++) warn_line(c, framed, &r->sorted[i]);
     for (size_t q = 0; q < r->n_packets; q++) {
         const sr_packet *p = &r->packets[q];
@@ -279,14 +332,16 @@ static int submit(sr_core *c, int slot, const uint8_t *framed, size_t nbytes) {
     return 0;
 }
 
-static int finish(sr_core *c, int slot, const uint8_t *framed) {
+static int finish(sr_core *c, int slot, const uint8_t *framed, size_t nbytes) {
     sr_pack_result r;
     int rc = sr_route_pack_result(c->ctx, slot, &r);
+    if (!rc && c->fail_finish && ++c->finishes == c->fail_finish) rc = -EIO;   /* fault injection */
     if (rc) {
         c->host_fills = 1;   /* the device's chain is no longer what the host holds */
+        c->dg_n[slot] = 0;
         return rc;
     }
-    complete(c, framed, &r);
+    complete(c, slot, framed, nbytes, &r);
     return 0;
 }
 
@@ -295,41 +350,88 @@ int sr_core_drain(sr_core *c) {
     if (c->in_flight < 0) return 0;
     const int slot = c->in_flight;
     c->in_flight = -1;
-    return finish(c, slot, c->in_flight_bytes);
+    return finish(c, slot, c->in_flight_bytes, c->in_flight_len);
 }
 
-int sr_core_submit(sr_core *c, int slot, size_t nbytes) {
+/* TRACE: the datagram ends of the batch about to go into `slot` (copied) */
+static int note_datagrams(sr_core *c, int slot, const uint32_t *ends, size_t n) {
+    c->dg_n[slot] = 0;
+    if (!c->trace || !n) return 0;
+    if (!ends) return -EINVAL;
+    if (n > c->dg_cap[slot]) {
+        uint32_t *p = realloc(c->dg_ends[slot], n * sizeof(uint32_t));
+        if (!p) return -ENOMEM;
+        c->dg_ends[slot] = p;
+        c->dg_cap[slot] = n;
+    }
+    memcpy(c->dg_ends[slot], ends, n * sizeof(uint32_t));
+    c->dg_n[slot] = n;
+    return 0;
+}
+
+int sr_core_submit_datagrams(sr_core *c, int slot, size_t nbytes, const uint32_t *ends, size_t n_datagrams) {
     if (!c || slot < 0 || slot > 1 || nbytes > c->max_batch) return -EINVAL;
     if (c->in_flight == slot) return -EBUSY;
     if (nbytes == 0) return 0;
     if (c->fail_submit && ++c->submits == c->fail_submit) return -EIO;   /* as a failed sr_route_pack_submit */
-    int rc = submit(c, slot, c->in[slot], nbytes);
-    if (rc) return rc;   /* nothing submitted: sr_core_in_flight() is not `slot` */
+    int rc = note_datagrams(c, slot, ends, n_datagrams);
+    if (rc) return rc;
+    if ((rc = submit(c, slot, c->in[slot], nbytes))) {
+        c->dg_n[slot] = 0;
+        return rc;   /* nothing submitted: sr_core_in_flight() is not `slot` */
+    }
     const int prev = c->in_flight;
     const uint8_t *prev_bytes = c->in_flight_bytes;
+    const size_t prev_len = c->in_flight_len;
     c->in_flight = slot;
     c->in_flight_bytes = c->in[slot];
+    c->in_flight_len = nbytes;
     if (prev < 0) return 0;
-    if ((rc = finish(c, prev, prev_bytes)) == 0) return 0;
+    if ((rc = finish(c, prev, prev_bytes, prev_len)) == 0) return 0;
     /* The previous batch failed, so its packets never reached the pending buffers the new batch's
      * device-chained fills assume: take the new batch back and route it again from the host's fills
      * (finish() set host_fills), so that host and device agree on every pending buffer. */
     sr_pack_result r;
-    (void)sr_route_pack_result(c->ctx, slot, &r);
+    const int rc_back = sr_route_pack_result(c->ctx, slot, &r);
+    if (rc_back && rc_back != -ENOSPC)
+        core_log(c, SR_ERROR, "%s: taking back the batch after a failed one failed %s", "udp_read_cb",
+                 strerror(-rc_back));
     c->in_flight = -1;
-    if (submit(c, slot, c->in[slot], nbytes) == 0) c->in_flight = slot;
+    if (submit(c, slot, c->in[slot], nbytes) == 0) c->in_flight = slot;   /* (its datagram ends kept) */
+    else c->dg_n[slot] = 0;
     return rc;
 }
 
+int sr_core_submit(sr_core *c, int slot, size_t nbytes) { return sr_core_submit_datagrams(c, slot, nbytes, NULL, 0); }
+
 int sr_core_in_flight(const sr_core *c) { return c ? c->in_flight : -EINVAL; }
 
-int sr_core_route(sr_core *c, const uint8_t *framed, size_t nbytes) {
+int sr_core_route_datagrams(sr_core *c, const uint8_t *framed, size_t nbytes, const uint32_t *ends,
+                            size_t n_datagrams) {
     if (!c || (nbytes && !framed) || nbytes > c->max_batch) return -EINVAL;
     int rc = sr_core_drain(c);
     if (rc) return rc;
     if (nbytes == 0) return 0;
-    if ((rc = submit(c, 0, framed, nbytes))) return rc;
-    return finish(c, 0, framed);
+    if ((rc = note_datagrams(c, 0, ends, n_datagrams))) return rc;
+    if ((rc = submit(c, 0, framed, nbytes))) {
+        c->dg_n[0] = 0;
+        return rc;
+    }
+    return finish(c, 0, framed, nbytes);
+}
+
+int sr_core_route(sr_core *c, const uint8_t *framed, size_t nbytes) {
+    return sr_core_route_datagrams(c, framed, nbytes, NULL, 0);
+}
+
+sr_ctx *sr_core_context(sr_core *c) { return c ? c->ctx : NULL; }
+
+int sr_core_inject_faults(sr_core *c, unsigned fail_submit, unsigned fail_finish) {
+    if (!c) return -EINVAL;
+    c->fail_submit = fail_submit;
+    c->fail_finish = fail_finish;
+    c->submits = c->finishes = 0;
+    return 0;
 }
 
 int sr_core_flush_timer(sr_core *c) {
@@ -361,7 +463,7 @@ int sr_core_ping(sr_core *c) {
     }
     if (pos > c->max_batch) return -ENOSPC;
     size_t nr = 0;
-    rc = sr_route_batch(c->ctx, b, pos, c->sorted, c->sorted_cap, &nr, NULL);
+    rc = sr_route_batch(c->ctx, b, pos, c->sorted, c->sorted_cap, &nr, c->trace ? c->ping_hash : NULL);
     if (rc) return rc;
     if (nr != c->n + 1) return -EIO;
     if ((rc = sr_last_probed_dead(c->ctx, c->probed))) return rc;
@@ -380,13 +482,15 @@ int sr_core_ping(sr_core *c) {
         const int n = snprintf(buf, sizeof(buf), "%s:%d|c\n%s:%d|c\n", d->traffic_metric, traffic, d->packet_metric,
                                packets);
         const uint16_t route = c->sorted[i].route; /* process_data_line, :231 */
+        if (c->trace) trace_line(c, buf, n, c->ping_hash[i], route);
+        else if (route >= c->n) core_log(c, SR_WARN, "%s: all downstreams are dead", "find_downstream");
         if (route < c->n) push(c, route, buf, (size_t)n);
-        else core_log(c, SR_WARN, "%s: all downstreams are dead", "find_downstream");
     }
     const int n = snprintf(buf, sizeof(buf), "%s:%d|g\n", c->alive_metric, count); /* :233-234 */
     const uint16_t route = c->sorted[c->n].route;
+    if (c->trace) trace_line(c, buf, n, c->ping_hash[c->n], route);
+    else if (route >= c->n) core_log(c, SR_WARN, "%s: all downstreams are dead", "find_downstream");
     if (route < c->n) push(c, route, buf, (size_t)n);
-    else core_log(c, SR_WARN, "%s: all downstreams are dead", "find_downstream");
     if (c->flush) c->flush(c->user);
     return 0;
 }

@@ -46,6 +46,10 @@ typedef struct data_thread {
     int slot;
     struct mmsghdr rmsg[RECV_VLEN];
     struct iovec riov[RECV_VLEN];
+    /* log_level TRACE: the framed datagrams' end offsets in the batch (sr_core_submit_datagrams) */
+    int trace;
+    uint32_t *ends;
+    size_t nends, ends_cap;
     /* egress: per outgoing socket, packets staged for one sendmmsg */
     int nout;
     struct mmsghdr *smsg;    /* [nout][SEND_VLEN] */
@@ -121,9 +125,10 @@ static void refresh_alive(data_thread *d) {
 static void submit_batch(data_thread *d) {
     if (!d->len) return;
     refresh_alive(d);
-    int rc = sr_core_submit(d->core, d->slot, d->len);
+    int rc = sr_core_submit_datagrams(d->core, d->slot, d->len, d->ends, d->nends);
     if (rc) sr_log(SR_ERROR, "%s: sr_core_submit() failed %s", "udp_read_cb", strerror(-rc));
     d->len = 0;
+    d->nends = 0;
     if (sr_core_in_flight(d->core) != d->slot) {
         /* the batch was not taken (its lines are lost, as the ERROR says): complete the one in
          * flight and keep filling this slot, which no GPU work reads */
@@ -195,6 +200,20 @@ static void udp_read_cb(struct ev_loop *loop, ev_io *w, int revents) {
             if (dst != src) memmove(dst, src, n);
             if (dst[n - 1] != '\n') dst[n++] = '\n';   /* sr-main.c:171-173 */
             d->len += n;
+            if (d->trace) {   /* "got packet" per datagram at TRACE (sr-main.c:174) */
+                if (d->nends == d->ends_cap) {
+                    const size_t nc = d->ends_cap ? 2 * d->ends_cap : 4096;
+                    uint32_t *p = realloc(d->ends, nc * sizeof(uint32_t));
+                    if (!p) {
+                        d->trace = 0;   /* the lines' own TRACE messages still follow */
+                        sr_log(SR_ERROR, "%s: malloc() failed %s", "udp_read_cb", strerror(errno));
+                        continue;
+                    }
+                    d->ends = p;
+                    d->ends_cap = nc;
+                }
+                d->ends[d->nends++] = (uint32_t)d->len;
+            }
         }
         if (k < RECV_VLEN) break;   /* drained */
     }
@@ -284,6 +303,7 @@ void *sr_data_thread(void *arg) {
     }
     d->slot = 0;
     d->batch = sr_core_slot_buffer(d->core, 0, &d->cap);
+    d->trace = sr_log_level <= SR_TRACE;
     d->nout = c->socket_out_num;
     d->sock_out = calloc((size_t)d->nout, sizeof(int));
     d->smsg = calloc((size_t)d->nout * SEND_VLEN, sizeof(struct mmsghdr));

@@ -360,6 +360,38 @@ typedef struct sr_pack_result {
 int sr_route_pack_submit(sr_ctx *ctx, int slot, const uint8_t *bytes, size_t nbytes, const uint16_t *fill);
 int sr_route_pack_result(sr_ctx *ctx, int slot, sr_pack_result *res);
 
+/* TRACE logging (log_level 0, the reference's default: sr-init.c:252). The reference logs, per line
+ * that reaches find_downstream, its sdbm hash and its first live pick (sr-main.c:91,102), so a router
+ * at that level needs every line's verdict, hash and shard in INPUT order. With sr_set_trace(ctx, 1)
+ * every later sr_route_pack_submit / sr_route_pack_batch also has the route kernel write each line's
+ * hash (0 for lines that fail the length or ':' test) and the copy-out kernel return the records in
+ * input order with the hashes; sr_route_pack_trace points at them after sr_route_pack_result(slot),
+ * valid until the slot is submitted again (slot 2: the last sr_route_pack_batch). Off by default: it
+ * costs 16 bytes per line of PCIe and host memory. Returns 0, -EINVAL, -EBUSY (not traced). */
+int sr_set_trace(sr_ctx *ctx, int on);
+int sr_route_pack_trace(sr_ctx *ctx, int slot, const sr_record **records, const uint64_t **hashes,
+                        size_t *n_records);
+
+/* Developer and test knobs of one context (A/B runs and tests only; the library reads no environment
+ * variable and no knob changes any record, packet or count, only which kernels produce them):
+ *   SR_KNOB_LB_SPIN       polls of a predecessor tile's tail granules before route_chunk_kernel
+ *                         computes the straddling line itself (default 65536; 0 always computes it);
+ *   SR_KNOB_DEFER_PICKS   first picks the route kernel makes before deferring a probe when two or
+ *                         more shards are dead (1 default, or 2);
+ *   SR_KNOB_MTU_CHUNK     packing chunk lines: 0 = by the launch's shape (default), 2048 or 4608;
+ *   SR_KNOB_MTU_XCD       1 (default): batches' packing chunks on one XCD from eight batches up;
+ *   SR_KNOB_MTU_WALK      1 (default): the chain walked inside mtu_emit up to 64 shards; 0: mtu_chain;
+ *   SR_KNOB_PERSIST       launches with every shard alive run the persistent chunk kernel: 0 never,
+ *                         1 in the chunk layout, 2 in every layout.
+ * Returns 0 or -EINVAL (unknown knob or value). */
+#define SR_KNOB_LB_SPIN 1
+#define SR_KNOB_DEFER_PICKS 2
+#define SR_KNOB_MTU_CHUNK 3
+#define SR_KNOB_MTU_XCD 4
+#define SR_KNOB_MTU_WALK 5
+#define SR_KNOB_PERSIST 6
+int sr_set_knob(sr_ctx *ctx, int knob, int64_t value);
+
 /* Page-locked host memory for the batches and outputs of the host-memory calls (their copies then
  * run at full link rate). NULL on failure. */
 void *sr_alloc_host(size_t bytes);

@@ -87,6 +87,28 @@ uint8_t *sr_core_slot_buffer(sr_core *core, int slot, size_t *capacity);
 int sr_core_submit(sr_core *core, int slot, size_t nbytes);
 int sr_core_drain(sr_core *core);
 
+/* The same two calls with the batch's datagram boundaries: ends[i] is the end offset (exclusive) of
+ * framed datagram i in the batch, ascending, the last = nbytes (empty datagrams have no entry: the
+ * reference logs nothing for them, sr-main.c:170). Only a core opened at log_level SR_TRACE reads
+ * them: it logs, in input order, "udp_read_cb: got packet ..." per datagram (sr-main.c:174) and, per
+ * line that reaches find_downstream, its hash and first live pick (sr-main.c:91,102) between the WARN
+ * lines, from the GPU's per-line hashes (sr_set_trace). Without boundaries (the calls above) a TRACE
+ * core logs the per-line messages only. The array is copied; it may be reused on return. */
+int sr_core_route_datagrams(sr_core *core, const uint8_t *framed, size_t nbytes, const uint32_t *ends,
+                            size_t n_datagrams);
+int sr_core_submit_datagrams(sr_core *core, int slot, size_t nbytes, const uint32_t *ends, size_t n_datagrams);
+
+/* The core's device context (sr_route.h), e.g. for sr_set_layout or sr_set_knob (developer A/B runs).
+ * Owned by the core. */
+sr_ctx *sr_core_context(sr_core *core);
+
+/* Test hook (fault injection; nothing calls it in the executable): the fail_submit-th call of
+ * sr_core_submit* fails as a failed sr_route_pack_submit (the batch is not taken), and the
+ * fail_finish-th batch to complete fails as a failed sr_route_pack_result (its packets and log lines
+ * are lost; a batch submitted after it on device-chained fills is taken back and routed again from
+ * the host's pending buffers). 0 = never. Counts start at this call. */
+int sr_core_inject_faults(sr_core *core, unsigned fail_submit, unsigned fail_finish);
+
 /* The slot whose batch is on the GPU (0 or 1), -1 if none, -EINVAL. After a failed sr_core_submit
  * it tells the caller whether the new batch was taken (the call can also fail after submitting it,
  * when completing the previous batch failed): a caller that refills the other slot only when

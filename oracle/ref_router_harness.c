@@ -17,8 +17,10 @@
  * (sr-main.c:21-46), i.e. a socket that is always writable; its sendto() goes to a UDP socket this
  * harness bound for that downstream (sa_in_data is re-pointed there; the metric names keep the
  * configured ports), and every datagram received is recorded with its downstream.
- * log_msg is intercepted with the linker's --wrap: WARN and ERROR messages are recorded as the
- * text the reference formats (without the timestamp / tid prefix of sr-util.c:23-24).
+ * log_msg is intercepted with the linker's --wrap: every message at or above the configured
+ * log_level (the reference's own test, sr-util.c:18-20) is recorded as the text the reference formats
+ * (without the timestamp / tid prefix of sr-util.c:23-24): WARN and ERROR at log_level 3, and also
+ * the TRACE lines of udp_read_cb / find_downstream at log_level 0 (sr-main.c:91,102,174).
  * gethostname is intercepted the same way so that the ping metric names are reproducible
  * (sr-init.c:298): it returns SR_TEST_HOSTNAME.
  *
@@ -26,7 +28,7 @@
  *   in : u32 tag: < 0xFFFFFF00 -> a datagram of that many bytes follows;
  *        0xFFFFFFF1 -> ceil(N/64) u64 alive words follow; 0xFFFFFFF2 flush tick; 0xFFFFFFF3 ping tick
  *   out: u8 1, u16 ds, u16 len, bytes           a packet sent to downstream ds
- *        u8 2, u8 level, u16 len, bytes         a WARN/ERROR message
+ *        u8 2, u8 level, u16 len, bytes         a log message (level >= log_level)
  *        u8 3, u16 ds, u16 len, bytes, u32 traffic, u32 packets   final pending buffer + counters
  */
 #include "sr-main.h" /* from /root/reference, via -I */
@@ -49,7 +51,7 @@ static void put(const void *p, size_t n) {
 }
 
 void __wrap_log_msg(int level, char *format, ...) {
-    if (level < WARN) return;
+    if (level < log_level) return;   /* sr-util.c:18-20 */
     char buf[1 << 14];
     va_list ap;
     va_start(ap, format);

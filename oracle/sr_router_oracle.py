@@ -2,9 +2,11 @@
 
 Pure-Python restatement of one reference data thread (hulu/statsd-router v0.0.16), line by line
 and in the reference's order, for small scripted sessions:
-  udp_read_cb        sr-main.c:149-191   framing, line split, length gate, WARN texts
+  udp_read_cb        sr-main.c:149-191   framing, line split, length gate, WARN texts, TRACE "got packet"
   process_data_line  sr-main.c:137-147   ':' verdict (hash via sr_oracle.hash_line, sr-main.c:120-134)
-  find_downstream    sr-main.c:86-117    probe, with the drop of every probed dead buffer (:106)
+  find_downstream    sr-main.c:86-117    probe, with the drop of every probed dead buffer (:106), TRACE
+                                         hash / pick lines (:91,102)
+  log_msg            sr-util.c:18-20     messages below the configured log_level are dropped
   push_to_downstream sr-main.c:73-83     1450-byte active buffer, flush when the line does not fit
   ds_schedule_flush  sr-main.c:49-71     packet and traffic counters (the ring never fills here:
                                          it is drained after every event, like the harness does)
@@ -26,9 +28,15 @@ def _int32(v: int) -> int:
     return v - (1 << 32) if v & 0x80000000 else v
 
 
+def _cstr(b: bytes) -> bytes:
+    """What printf's %s / %.*s prints of b: up to its first NUL."""
+    return b.split(b"\0", 1)[0]
+
+
 class DataThread:
-    def __init__(self, n, ds_hosts, ds_data_ports, ping_prefix, hostname, data_port):
+    def __init__(self, n, ds_hosts, ds_data_ports, ping_prefix, hostname, data_port, log_level=3):
         self.n = n
+        self.log_level = log_level
         self.alive = [0] * n                      # health clients start dead (sr-init.c:85)
         self.pending = [b""] * n
         self.traffic = [0] * n
@@ -50,8 +58,12 @@ class DataThread:
             self.packet_name.append(b"%s.%s-%s.packets" % (p, name, port))
 
     # ---- the reference functions ------------------------------------------------------------
+    def _log(self, level: int, text: bytes):   # log_msg (sr-util.c:18-20)
+        if level >= self.log_level:
+            self.logs.append((level, text))
+
     def _warn(self, text: bytes):
-        self.logs.append((3, text))
+        self._log(3, text)
 
     def _flush(self, s):                          # ds_schedule_flush
         self.npackets[s] += 1
@@ -65,11 +77,13 @@ class DataThread:
         self.pending[s] += line
 
     def _find_downstream(self, h: int, line: bytes):
+        self._log(0, b"find_downstream: hash = %x, length = %d, line = " % (h, len(line)) + _cstr(line))   # :91
         idx = list(range(self.n))
         for i in range(self.n, 0, -1):
             j = h % i
             k = idx[j]
             if self.alive[k]:
+                self._log(0, b"find_downstream: pushing to downstream %d" % k)                        # :102
                 self._push(k, line)
                 return
             self.pending[k] = b""                  # :106
@@ -81,19 +95,21 @@ class DataThread:
     def _process_data_line(self, line: bytes):
         h = O.hash_line(line)
         if h is None:
-            self._warn(b"process_data_line: invalid metric " + line[:-1].split(b"\0", 1)[0])
+            self._warn(b"process_data_line: invalid metric " + _cstr(line[:-1]))
             return
         self._find_downstream(h, line)
 
     def datagram(self, d: bytes):                 # udp_read_cb
         buf = O.frame(d)
+        if buf:
+            self._log(0, b"udp_read_cb: got packet " + _cstr(buf))                                   # :174
         while buf:
             k = buf.index(b"\n") + 1
             line, buf = buf[:k], buf[k:]
             if 5 < len(line) < CAP:
                 self._process_data_line(line)
             else:
-                self._warn(b"udp_read_cb: invalid length %d of metric " % len(line) + line.split(b"\0", 1)[0])
+                self._warn(b"udp_read_cb: invalid length %d of metric " % len(line) + _cstr(line))
 
     def set_alive(self, alive):
         self.alive = [int(a) for a in alive]

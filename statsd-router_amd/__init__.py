@@ -52,10 +52,13 @@ ABI_FUNCTIONS = (
     "sr_pack_many_by_owner", "sr_pack_packets", "sr_pack_packets_many", "sr_route_pack_batch", "sr_alloc_host", "sr_free_host", "sr_sync", "sr_close", "sr_version",
     "sr_comm_id", "sr_comm_open", "sr_comm_close", "sr_exchange_sizes", "sr_exchange_data",
     "sr_exchange_plan", "sr_exchange_run", "sr_exchange_rebase", "sr_route_pack_submit", "sr_route_pack_result",
+    "sr_set_trace", "sr_route_pack_trace", "sr_set_knob",
 )
 SR_MAX_PACK_DOWNSTREAMS = 4096
 SR_LAYOUT_AUTO, SR_LAYOUT_UNIFORM, SR_LAYOUT_SEGMENTS, SR_LAYOUT_CHUNKS = 0, 1, 2, 3
 SR_COMM_ID_BYTES = 128
+# sr_set_knob (developer / test knobs of one context; none changes a result)
+SR_KNOB_LB_SPIN, SR_KNOB_DEFER_PICKS, SR_KNOB_MTU_CHUNK, SR_KNOB_MTU_XCD, SR_KNOB_MTU_WALK, SR_KNOB_PERSIST = 1, 2, 3, 4, 5, 6
 LAYOUT_NAMES = {0: "none", 1: "uniform", 2: "segments", 3: "chunks"}
 PACKET_DTYPE = np.dtype([("first", "<u4"), ("nlines", "<u2"), ("shard", "<u2"), ("length", "<u2"),
                          ("carry", "<u2"), ("open", "<u4")])
@@ -194,6 +197,9 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_exchange_rebase": (ctypes.c_int, [vp, vp, vp, ctypes.c_int]),
         "sr_route_pack_submit": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_size_t, vp]),
         "sr_route_pack_result": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(SrPackResult)]),
+        "sr_set_trace": (ctypes.c_int, [vp, ctypes.c_int]),
+        "sr_route_pack_trace": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), c_size_p]),
+        "sr_set_knob": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int64]),
     }
     for name in ABI_FUNCTIONS:
         fn = getattr(lib, name)  # raises AttributeError if the export is missing
@@ -337,6 +343,27 @@ class Router:
         """sr_set_layout: SR_LAYOUT_AUTO (default), SR_LAYOUT_UNIFORM, SR_LAYOUT_SEGMENTS or
         SR_LAYOUT_CHUNKS (the route kernel's lane layout; records are identical either way)."""
         _check(self._lib.sr_set_layout(self._h, int(layout)), "sr_set_layout")
+
+    def set_knob(self, knob: int, value: int) -> None:
+        """sr_set_knob: a developer / test knob of this context (SR_KNOB_*); results never change."""
+        _check(self._lib.sr_set_knob(self._h, int(knob), int(value)), "sr_set_knob")
+
+    def set_trace(self, on: bool = True) -> None:
+        """sr_set_trace: later route + pack submissions also return input-order records and hashes."""
+        _check(self._lib.sr_set_trace(self._h, 1 if on else 0), "sr_set_trace")
+
+    def route_pack_trace(self, slot: int):
+        """sr_route_pack_trace after route_pack_result(slot) (slot 2: the last route_pack): (records in
+        input order, per-line hashes), copied."""
+        r, h, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_size_t()
+        _check(self._lib.sr_route_pack_trace(self._h, slot, ctypes.byref(r), ctypes.byref(h), ctypes.byref(n)),
+               "sr_route_pack_trace")
+        k = n.value
+        if not k:
+            return np.zeros(0, RECORD_DTYPE), np.zeros(0, np.uint64)
+        recs = np.frombuffer((ctypes.c_uint8 * (8 * k)).from_address(r.value), dtype=RECORD_DTYPE).copy()
+        hs = np.frombuffer((ctypes.c_uint8 * (8 * k)).from_address(h.value), dtype=np.uint64).copy()
+        return recs, hs
 
     def last_layout(self) -> int:
         """sr_last_layout: the lane layout of the context's last route launch (1 uniform, 2 segments,

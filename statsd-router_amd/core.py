@@ -61,6 +61,13 @@ def router_lib() -> ctypes.CDLL:
         L.sr_core_metric_name.restype = ctypes.c_char_p
         L.sr_core_metric_name.argtypes = [vp, ctypes.c_uint32, ctypes.c_int]
         L.sr_core_close.restype, L.sr_core_close.argtypes = None, [vp]
+        L.sr_core_route_datagrams.restype = ctypes.c_int
+        L.sr_core_route_datagrams.argtypes = [vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t]
+        L.sr_core_submit_datagrams.restype = ctypes.c_int
+        L.sr_core_submit_datagrams.argtypes = [vp, ctypes.c_int, ctypes.c_size_t, vp, ctypes.c_size_t]
+        L.sr_core_context.restype, L.sr_core_context.argtypes = vp, [vp]
+        L.sr_core_inject_faults.restype = ctypes.c_int
+        L.sr_core_inject_faults.argtypes = [vp, ctypes.c_uint, ctypes.c_uint]
         _RLIB = L
     return _RLIB
 
@@ -113,20 +120,33 @@ class Core:
         w = np.ascontiguousarray(alive_words(self.n, alive))
         _check(self._L.sr_core_set_alive(self._h, w.ctypes.data), "sr_core_set_alive")
 
-    def route(self, framed: bytes) -> None:
-        buf = ctypes.create_string_buffer(bytes(framed), max(len(framed), 1))
-        _check(self._L.sr_core_route(self._h, buf, len(framed)), "sr_core_route")
+    @staticmethod
+    def _ends(ends):
+        """Datagram end offsets as a u32 array (None: no boundaries)."""
+        if ends is None:
+            return None, 0
+        a = np.ascontiguousarray(np.asarray(ends, dtype=np.uint32))
+        return a, int(a.size)
 
-    def route_in_place(self, framed: bytes) -> None:
+    def route(self, framed: bytes, ends=None) -> None:
+        """sr_core_route (ends: the framed datagrams' end offsets, for TRACE: sr_core_route_datagrams)."""
+        buf = ctypes.create_string_buffer(bytes(framed), max(len(framed), 1))
+        a, n = self._ends(ends)
+        _check(self._L.sr_core_route_datagrams(self._h, buf, len(framed), a.ctypes.data if n else None, n),
+               "sr_core_route")
+
+    def route_in_place(self, framed: bytes, ends=None) -> None:
         """Frame into the core's page-locked batch buffer first (what a C caller does)."""
         cap = ctypes.c_size_t()
         p = self._L.sr_core_batch_buffer(self._h, ctypes.byref(cap))
         if len(framed) > cap.value:
             raise SrError(28, "batch larger than the core's buffer")
         ctypes.memmove(p, bytes(framed), len(framed))
-        _check(self._L.sr_core_route(self._h, p, len(framed)), "sr_core_route")
+        a, n = self._ends(ends)
+        _check(self._L.sr_core_route_datagrams(self._h, p, len(framed), a.ctypes.data if n else None, n),
+               "sr_core_route")
 
-    def submit(self, framed: bytes) -> None:
+    def submit(self, framed: bytes, ends=None) -> None:
         """Double-buffered: frame into the next slot's buffer and sr_core_submit it (the previous
         batch completes here, the new one stays in flight until the next submit or drain)."""
         slot = getattr(self, "_slot", 0)
@@ -135,8 +155,19 @@ class Core:
         if len(framed) > cap.value:
             raise SrError(28, "batch larger than the core's buffer")
         ctypes.memmove(p, bytes(framed), len(framed))
-        _check(self._L.sr_core_submit(self._h, slot, len(framed)), "sr_core_submit")
-        self._slot = slot ^ 1
+        a, n = self._ends(ends)
+        rc = self._L.sr_core_submit_datagrams(self._h, slot, len(framed), a.ctypes.data if n else None, n)
+        if self._L.sr_core_in_flight(self._h) == slot:
+            self._slot = slot ^ 1   # taken, even when completing the previous batch failed
+        _check(rc, "sr_core_submit")
+
+    def inject_faults(self, fail_submit: int = 0, fail_finish: int = 0) -> None:
+        """sr_core_inject_faults (test hook)."""
+        _check(self._L.sr_core_inject_faults(self._h, fail_submit, fail_finish), "sr_core_inject_faults")
+
+    def set_layout(self, layout: int) -> None:
+        """sr_set_layout on the core's device context (sr_core_context)."""
+        _check(lib().sr_set_layout(self._L.sr_core_context(self._h), int(layout)), "sr_set_layout")
 
     def in_flight(self) -> int:
         """sr_core_in_flight: the slot whose batch is on the GPU, or -1."""

@@ -910,6 +910,10 @@ struct PackOut {
     uint16_t *h_fill;
     uint64_t *h_probed;
     uint64_t *h_counts;
+    const sr_record *recs;       // sr_set_trace (else null): the records in input order and the hashes
+    const uint64_t *hashes;
+    sr_record *h_recs;
+    uint64_t *h_hashes;
 };
 
 __global__ __launch_bounds__(256) void pack_out_kernel(PackOut o) {
@@ -926,6 +930,12 @@ __global__ __launch_bounds__(256) void pack_out_kernel(PackOut o) {
     for (uint64_t i = tid; i < o.nds; i += stride) o.h_fill[i] = o.fill[i];
     for (uint64_t i = tid; i < o.nwords; i += stride) o.h_probed[i] = o.probed ? o.probed[i] : 0ull;
     if (tid < 3) o.h_counts[tid] = o.counts[tid];
+    if (o.recs) {   // TRACE: input-order records and per-line hashes (sr_route_pack_trace)
+        for (uint64_t i = tid; i < nr; i += stride) {
+            o.h_recs[i] = o.recs[i];
+            o.h_hashes[i] = o.hashes[i];
+        }
+    }
 }
 
 }  // namespace srk

@@ -12,7 +12,7 @@
 #include <utility>
 #include <vector>
 
-#include "chunk_kernel.hpp"
+#include "persist_kernel.hpp"
 
 namespace srk {
 
@@ -73,7 +73,7 @@ struct DeviceState {
     uint64_t *d_kpow = nullptr;
     uint64_t *d_cpow = nullptr;          // route_chunk_kernel's power tables (kCpowEntries)
     uint64_t *d_tail = nullptr;          // route_chunk_kernel's tail granules, 4 per tile
-    uint32_t lb_spin = 1u << 16;         // its look-back polls before computing a line itself
+    uint32_t lb_spin = 1u << 16;         // its look-back polls before computing a line itself (SR_KNOB_LB_SPIN)
     Control *d_ctl = nullptr;
     uint64_t *d_status = nullptr;
     uint64_t *d_bases = nullptr;
@@ -93,12 +93,15 @@ struct DeviceState {
     // picks the route kernel makes before deferring a probe (RouteParams::picks) when the deferred
     // probes run anyway (two or more dead shards): 1 (measured: C4 / C5 with 25 % dead 1-2 % faster
     // than 2; with one dead shard nothing is deferred at 2 picks, and deferring a quarter of the
-    // lines cost C2 +30 %); SR_DEFER_PICKS=2 overrides
+    // lines cost C2 +30 %); SR_KNOB_DEFER_PICKS = 2 overrides (sr_set_knob)
     uint32_t defer_picks = 1;
+    // SR_KNOB_PERSIST: all-alive launches in the chunk layout (1), or in any layout (2), run the
+    // persistent kernel (route_persist_kernel); 0: never
+    uint32_t persist = 0;
+    uint32_t persist_slots = 0;      // resident route_persist_kernel workgroups on the device (0: not yet asked)
 
     int init(size_t max_batch_bytes, uint32_t n_downstreams) {
         max_batch = max_batch_bytes;
-        if (const char *e = getenv("SR_DEFER_PICKS")) defer_picks = atoi(e) == 2 ? 2u : 1u;
         nds = n_downstreams;
         nwords = (n_downstreams + 63) / 64;
         // status granules for kMaxBatches batches of the smallest tile (256 threads, 16 KiB)
@@ -111,11 +114,6 @@ struct DeviceState {
         if (hipMalloc(&d_cpow, kCpowEntries * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&d_tail, (max_tiles ? max_tiles : 1) * 4 * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
         if (hipMemset(d_tail, 0, (max_tiles ? max_tiles : 1) * 4 * sizeof(uint64_t)) != hipSuccess) return -EIO;
-        if (const char *e = getenv("SR_LB_SPIN")) lb_spin = (uint32_t)strtoul(e, nullptr, 0);
-        if (const char *e = getenv("SR_LAYOUT")) {   // the context's initial layout (tests run every layout)
-            const int v = atoi(e);
-            if (v >= SR_LAYOUT_AUTO && v <= SR_LAYOUT_CHUNKS) layout_mode = v;
-        }
         if (hipMalloc(&d_ctl, sizeof(Control)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&d_status, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
         if (hipMalloc(&d_bases, (max_tiles ? max_tiles : 1) * sizeof(uint64_t)) != hipSuccess) return -ENOMEM;
@@ -195,38 +193,45 @@ struct DeviceState {
     }
 
     int set_alive(const uint64_t *alive, hipStream_t stream) {
+        // The snapshot's scratch first, so that a failure leaves the context's state as it was
         uint32_t live = 0;
         for (uint32_t w = 0; w < nwords; ++w) {
             uint64_t v = alive[w];
             if (w == nwords - 1 && (nds & 63)) v &= (1ull << (nds & 63)) - 1;
-            h_alive[w] = v;
             live += (uint32_t)__builtin_popcountll(v);
         }
-        dead = nds - live;
-        if (nwords && hipMemcpyAsync(d_alive, h_alive, nwords * sizeof(uint64_t), hipMemcpyHostToDevice, stream) !=
-                          hipSuccess)
-            return -EIO;
-        if (dead > (uint32_t)kOverlay && !d_pending) {
-            pending_cap = (uint32_t)(max_batch / SR_MIN_LINE_LENGTH + 1);
-            if (hipMalloc(&d_pending, (size_t)pending_cap * sizeof(PendingLine)) != hipSuccess) {
+        const uint32_t ndead = nds - live;
+        if (ndead > (uint32_t)kOverlay && !d_pending) {
+            const uint32_t cap = (uint32_t)(max_batch / SR_MIN_LINE_LENGTH + 1);
+            if (hipMalloc(&d_pending, (size_t)cap * sizeof(PendingLine)) != hipSuccess) {
                 d_pending = nullptr;
-                pending_cap = 0;
                 return -ENOMEM;
             }
+            pending_cap = cap;
         }
         // two or more dead: the deferred probes keep hashes by record index; sized here for a batch
         // of max_batch bytes (the router's one-batch launches), so that a data thread's launches never
         // reallocate (hipFree / hipMalloc synchronise the device) in the middle of its stream
-        if (dead >= 2 && dead < nds) {
+        if (ndead >= 2 && ndead < nds) {
             const int rc = reserve_defer(max_batch / SR_MIN_LINE_LENGTH + 1);
             if (rc) return rc;
         }
-        if (dead && dead < nds && nds <= 64 * kAliveLds && !d_tile_pd &&
+        if (ndead && ndead < nds && nds <= 64 * kAliveLds && !d_tile_pd &&
             hipMalloc(&d_tile_pd, (size_t)(max_tiles ? max_tiles : 1) * nwords * sizeof(uint64_t)) != hipSuccess) {
             d_tile_pd = nullptr;   // the launches replay the probes instead
         }
-        // the copy reads h_alive: complete it before the snapshot can change again
-        return hipStreamSynchronize(stream) == hipSuccess ? 0 : -EIO;
+        for (uint32_t w = 0; w < nwords; ++w) {
+            uint64_t v = alive[w];
+            if (w == nwords - 1 && (nds & 63)) v &= (1ull << (nds & 63)) - 1;
+            h_alive[w] = v;
+        }
+        dead = ndead;
+        const bool copied = !nwords || hipMemcpyAsync(d_alive, h_alive, nwords * sizeof(uint64_t),
+                                                      hipMemcpyHostToDevice, stream) == hipSuccess;
+        // the copy reads h_alive: complete it before the snapshot can change again (also after a
+        // failed enqueue, so that nothing can still be reading h_alive)
+        const bool synced = hipStreamSynchronize(stream) == hipSuccess;
+        return copied && synced ? 0 : -EIO;
     }
 
     int reserve_defer(size_t entries) {
@@ -430,7 +435,31 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
         }
     }
     if (ds.wide() && hipMemsetAsync(&ds.d_ctl->pending, 0, sizeof(uint32_t), stream) != hipSuccess) return -EIO;
-    if constexpr ((ABL & KV_CHUNKS) != 0) {
+    if constexpr ((ABL & KV_PERSIST) != 0) {
+        // one workgroup per resident slot (4 per CU), the scanners' slots included: per XCD class the
+        // slots of its XCD less the scanners placed there (block b runs on XCD b % 8)
+        if (!ds.persist_slots) {
+            int occ = 0, cus = 0, dev = 0;
+            (void)hipGetDevice(&dev);
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)route_persist_kernel<ABL>, BLOCK, 0) !=
+                    hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || occ <= 0 ||
+                cus <= 0)
+                return -EIO;
+            ds.persist_slots = (uint32_t)(occ * cus);
+        }
+        uint32_t workers;
+        if (xl) {
+            const uint32_t per_xcd = ds.persist_slots / 8u, scan_xcd = (p.nb + 7u) / 8u;
+            p.pworkers = per_xcd > scan_xcd + 1u ? per_xcd - scan_xcd : 1u;
+            workers = 8u * p.pworkers;
+        } else {
+            p.pworkers = ds.persist_slots > p.nb + 1u ? ds.persist_slots - p.nb : 1u;
+            workers = p.pworkers;
+        }
+        p.total_blocks = p.nb + workers;
+        hipLaunchKernelGGL((route_persist_kernel<ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
+    } else if constexpr ((ABL & KV_CHUNKS) != 0) {
         static_assert(BLOCK == 256, "route_chunk_kernel: 256 lanes of 64 bytes per 16 KiB tile");
         // its probe stops after the first picks: with two or more dead shards it needs the deferral
         // (no scratch for it, e.g. inside a stream capture: the uniform kernel probes in full)

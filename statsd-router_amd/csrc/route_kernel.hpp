@@ -199,6 +199,7 @@ struct RouteParams {
     const uint64_t *cpow;
     uint64_t *tail;
     uint32_t lb_spin;
+    uint32_t pworkers;       // route_persist_kernel: workgroups per XCD class (persist_kernel.hpp)
     // per XCD class c, its batches in tile order: (class-local end tile << 6) | batch index;
     // ~0u after the last (one scalar load finds a tile's batch)
     uint32_t cls_tab[8][kPerClass];

@@ -53,6 +53,10 @@ struct sr_ctx {
     uint16_t *d_fill;             // [3][nds]: two chained outputs, then the uploaded fill of a submission
     int fill_cur;                 // region of d_fill holding the last submission's output (0 or 1)
     uint64_t *d_mcounts;          // 3 u64
+    int trace;                    // sr_set_trace: submissions also return input-order records + hashes
+    // packing knobs (sr_set_knob): forced chunk lines (0: by shape), XCD-local chunks, chain walked in emit
+    uint32_t mtu_chunk;
+    int mtu_xcd, mtu_walk;
     // page-locked, device-mapped outputs of sr_route_pack_submit: slots 0 and 1, slot 2 is
     // sr_route_pack_batch's own
     struct Slot {
@@ -65,6 +69,10 @@ struct sr_ctx {
         sr_packet *packets;
         uint16_t *fill, *fill_in;
         uint64_t *probed, *counts;
+        // sr_set_trace: input-order records and per-line hashes (one more page-locked allocation)
+        uint8_t *thost, *tdev;
+        size_t trec_cap;
+        int traced;               // the batch in the slot was submitted with trace on
     } slot[3];
 };
 
@@ -80,6 +88,11 @@ static void free_ptr(void *p) { (void)hipFree(p); }
 // never the shipped library): SR_VARIANT in the environment then selects one.
 static int launch_product(DeviceState &ds, const RouteParams &p, hipStream_t stream) {
     const bool seg = ds.choose_segments(stream);
+    // every shard alive, persistent chunk kernel asked for (SR_KNOB_PERSIST)
+    if (ds.dead == 0 && ds.persist && !seg && (ds.persist == 2 || ds.last_layout == SR_LAYOUT_CHUNKS)) {
+        ds.last_layout = SR_LAYOUT_CHUNKS;
+        return launch_route<kBlock, KV_CHUNKS | KV_ALIVE | KV_PERSIST>(ds, p, stream);
+    }
     if (ds.last_layout == SR_LAYOUT_CHUNKS) {
         if (ds.dead == 0) return launch_route<kBlock, KV_CHUNKS | KV_ALIVE | SR_CHUNK_ABL>(ds, p, stream);
         return launch_route<kBlock, KV_CHUNKS | SR_CHUNK_ABL>(ds, p, stream);
@@ -177,6 +190,7 @@ void sr_close(sr_ctx *c) {
     free_ptr(c->d_mcounts);
     for (auto &sl : c->slot) {
         if (sl.host) (void)hipHostFree(sl.host);
+        if (sl.thost) (void)hipHostFree(sl.thost);
         if (sl.done) (void)hipEventDestroy(sl.done);
     }
     if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -195,6 +209,8 @@ int sr_open(sr_ctx **out, int device, size_t max_batch_bytes, uint32_t n_downstr
     if (!c) return -ENOMEM;
     new (&c->ds) DeviceState();
     c->device = device;
+    c->mtu_xcd = 1;
+    c->mtu_walk = 1;
     int rc = -ENOMEM;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) goto fail;
     c->stream = c->own_stream;
@@ -230,6 +246,41 @@ int sr_set_layout(sr_ctx *c, int layout) {
 }
 
 int sr_last_layout(const sr_ctx *c) { return c ? c->ds.last_layout : -EINVAL; }
+
+int sr_set_knob(sr_ctx *c, int knob, int64_t v) {
+    if (!c) return -EINVAL;
+    switch (knob) {
+    case SR_KNOB_LB_SPIN:
+        if (v < 0 || v > 0xFFFFFFFFll) return -EINVAL;
+        c->ds.lb_spin = (uint32_t)v;
+        return 0;
+    case SR_KNOB_DEFER_PICKS:
+        if (v != 1 && v != 2) return -EINVAL;
+        c->ds.defer_picks = (uint32_t)v;
+        return 0;
+    case SR_KNOB_MTU_CHUNK:
+        if (v != 0 && v != kMtuChunkSmall && v != kMtuChunk) return -EINVAL;
+        c->mtu_chunk = (uint32_t)v;
+        return 0;
+    case SR_KNOB_PERSIST:
+        if (v < 0 || v > 2) return -EINVAL;
+        c->ds.persist = (uint32_t)v;
+        return 0;
+    case SR_KNOB_MTU_XCD:
+    case SR_KNOB_MTU_WALK:
+        if (v != 0 && v != 1) return -EINVAL;
+        (knob == SR_KNOB_MTU_XCD ? c->mtu_xcd : c->mtu_walk) = (int)v;
+        return 0;
+    default:
+        return -EINVAL;
+    }
+}
+
+int sr_set_trace(sr_ctx *c, int on) {
+    if (!c) return -EINVAL;
+    c->trace = on ? 1 : 0;
+    return 0;
+}
 
 int sr_sync(sr_ctx *c) {
     if (!c) return -EINVAL;
@@ -407,13 +458,9 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     // flight (2048 lines: 16 KiB of LDS per table workgroup, ten per CU instead of five).
     uint64_t all_records = 0;
     for (size_t j = 0; j < count; ++j) all_records += batches[j].max_records;
-    static const int ch_env = [] {   // developer A/B: SR_MTU_CH=2048 / 4096 forces the chunk size
-        const char *e = getenv("SR_MTU_CH");
-        return e ? atoi(e) : 0;
-    }();
     uint32_t ch = all_records <= (uint64_t)(nds ? nds : 1) * 32u * kMtuChunk ? (uint32_t)kMtuChunkSmall
                                                                             : (uint32_t)kMtuChunk;
-    if (ch_env == kMtuChunkSmall || ch_env == kMtuChunk) ch = (uint32_t)ch_env;
+    if (c->mtu_chunk) ch = c->mtu_chunk;   // SR_KNOB_MTU_CHUNK (A/B runs)
     uint32_t tiles = 0, chunks = 0;
     for (size_t j = 0; j < count; ++j) {
         const sr_pack_batch &b = batches[j];
@@ -473,12 +520,8 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
 #endif
     // the chunk kernels' grid: eight batches or more put each batch's chunks on one XCD
     // (mtu_chunk_slot): eight times the most slots any XCD takes
-    static const bool xcd_env = [] {   // developer A/B: SR_MTU_XCD=0 deals the chunks in launch order
-        const char *e = getenv("SR_MTU_XCD");
-        return !(e && e[0] == '0');
-    }();
     uint32_t chunk_grid = chunks;
-    L.xcd = (xcd_env && count >= 8) ? 1u : 0u;
+    L.xcd = (c->mtu_xcd && count >= 8) ? 1u : 0u;   // SR_KNOB_MTU_XCD 0: chunks dealt in launch order
     if (L.xcd) {
         uint32_t per[8] = {0, 0, 0, 0, 0, 0, 0, 0}, mx = 0;
         for (size_t j = 0; j < count; ++j) {
@@ -501,13 +544,9 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     else
         hipLaunchKernelGGL(mtu_table_kernel<kMtuChunkSmall>, dim3(chunk_grid), dim3(kMtuTableBlock), 0, c->stream, L);
     // the chain inside the emit kernel (one lane per shard) up to 64 shards, else mtu_chain
-    static const bool walk_env = [] {   // developer A/B: SR_MTU_WALK=0 keeps mtu_chain
-        const char *e = getenv("SR_MTU_WALK");
-        return !(e && e[0] == '0');
-    }();
     // (a batch's fill_out read as some batch's fill_in would change under the walks: mtu_chain reads
     // every fill_in before the shard's fill_out is written)
-    bool walk = walk_env && nds <= 64;
+    bool walk = c->mtu_walk && nds <= 64;   // SR_KNOB_MTU_WALK 0: mtu_chain
     for (size_t a = 0; walk && a < count; ++a)
         for (size_t b = 0; walk && b < count; ++b) {
             const uint16_t *in = batches[b].d_fill_in, *out = batches[a].d_fill_out;
@@ -579,6 +618,27 @@ static int slot_reserve(sr_ctx *c, int k, size_t nbytes) {
     return 0;
 }
 
+// sr_set_trace: the slot's input-order records and hashes (grown, never shrunk; the slot is idle)
+static int slot_trace_reserve(sr_ctx *c, int k, size_t nbytes) {
+    sr_ctx::Slot &sl = c->slot[k];
+    if (sl.thost && nbytes <= sl.trec_cap) return 0;
+    if (sl.thost) (void)hipHostFree(sl.thost);
+    sl.thost = sl.tdev = nullptr;
+    sl.trec_cap = 0;
+    void *h = nullptr, *d = nullptr;
+    if (hipHostMalloc(&h, up256(nbytes * sizeof(sr_record)) + nbytes * sizeof(uint64_t) + 8, hipHostMallocMapped) !=
+        hipSuccess)
+        return -ENOMEM;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+        (void)hipHostFree(h);
+        return -EIO;
+    }
+    sl.thost = (uint8_t *)h;
+    sl.tdev = (uint8_t *)d;
+    sl.trec_cap = nbytes;
+    return 0;
+}
+
 static int pack_submit(sr_ctx *c, int k, const uint8_t *bytes, size_t nbytes, const uint16_t *fill) {
     sr_ctx::Slot &sl = c->slot[k];
     if (sl.busy) return -EBUSY;
@@ -593,6 +653,7 @@ static int pack_submit(sr_ctx *c, int k, const uint8_t *bytes, size_t nbytes, co
     // data thread while its socket fills
     const size_t full = c->ds.max_batch, fullp = (size_t)SR_MAX_PACKETS(full, nds);
     if ((rc = slot_reserve(c, k, full))) return rc;
+    if (c->trace && (rc = slot_trace_reserve(c, k, full))) return rc;
     const size_t cap = nbytes ? nbytes : 1;   // never more lines than bytes
     const size_t pcap = (size_t)SR_MAX_PACKETS(cap, nds);
     if ((rc = grow((void **)&c->d_out, &c->d_out_cap, full, sizeof(sr_record)))) return rc;
@@ -623,8 +684,9 @@ static int pack_submit(sr_ctx *c, int k, const uint8_t *bytes, size_t nbytes, co
         // over 1024 shards with some dead the route kernel also writes the hashes: the probed-dead
         // replay then reads 8 bytes per line instead of re-hashing the names (probed_dead_kernel);
         // up to 1024 the probes note the dead shards themselves
+        // TRACE (sr_set_trace) needs every line's hash too (sr-main.c:91)
         uint64_t *hashes = nullptr;
-        if (c->ds.replay_wants_hashes()) {
+        if (c->trace || c->ds.replay_wants_hashes()) {
             if ((rc = grow((void **)&c->d_hash, &c->d_hash_cap, full, sizeof(uint64_t)))) return rc;
             hashes = c->d_hash;
         }
@@ -651,6 +713,11 @@ static int pack_submit(sr_ctx *c, int k, const uint8_t *bytes, size_t nbytes, co
     o.h_fill = (uint16_t *)(sl.dev + ((uint8_t *)sl.fill - sl.host));
     o.h_probed = (uint64_t *)(sl.dev + ((uint8_t *)sl.probed - sl.host));
     o.h_counts = (uint64_t *)(sl.dev + ((uint8_t *)sl.counts - sl.host));
+    sl.traced = c->trace;
+    o.recs = (c->trace && nbytes) ? c->d_out : nullptr;   // input order, and the hashes (sr_route_pack_trace)
+    o.hashes = (c->trace && nbytes) ? c->d_hash : nullptr;
+    o.h_recs = c->trace ? (sr_record *)sl.tdev : nullptr;
+    o.h_hashes = c->trace ? (uint64_t *)(sl.tdev + up256(sl.trec_cap * sizeof(sr_record))) : nullptr;
     // one workgroup per 512 records (two per thread), at most 1024 workgroups (grid-stride beyond)
     const uint64_t want = (cap + 511) / 512;
     hipLaunchKernelGGL(pack_out_kernel, dim3((uint32_t)(want < 1024 ? (want ? want : 1) : 1024)), dim3(256), 0,
@@ -676,6 +743,17 @@ static int pack_result(sr_ctx *c, int k, sr_pack_result *res) {
     res->n_valid = (size_t)(nv < res->n_records ? nv : res->n_records);
     res->n_packets = (size_t)(np < sl.pk_cap ? np : sl.pk_cap);
     return (nr > sl.rec_cap || np > sl.pk_cap) ? -ENOSPC : 0;
+}
+
+int sr_route_pack_trace(sr_ctx *c, int slot, const sr_record **records, const uint64_t **hashes, size_t *n) {
+    if (!c || !records || !hashes || !n || slot < 0 || slot > 2) return -EINVAL;
+    const sr_ctx::Slot &sl = c->slot[slot];
+    if (sl.busy || !sl.traced || !sl.thost || !sl.counts) return -EBUSY;
+    const uint64_t nr = sl.counts[2];
+    *n = (size_t)(nr < sl.trec_cap ? nr : sl.trec_cap);
+    *records = (const sr_record *)sl.thost;
+    *hashes = (const uint64_t *)(sl.thost + up256(sl.trec_cap * sizeof(sr_record)));
+    return 0;
 }
 
 int sr_route_pack_submit(sr_ctx *c, int slot, const uint8_t *bytes, size_t nbytes, const uint16_t *fill) {

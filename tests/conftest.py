@@ -22,7 +22,35 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def pkg():
-    return importlib.import_module("statsd-router_amd")
+    m = importlib.import_module("statsd-router_amd")
+    _force_layout(m)
+    return m
+
+
+def _force_layout(m):
+    """SR_TEST_LAYOUT=<n> (test runs only): every context the tests open starts in lane layout n
+    (sr_set_layout), e.g. the parity, MTU and router-core suites all in the chunk layout (3). The
+    library itself reads no environment variable."""
+    lay = os.environ.get("SR_TEST_LAYOUT")
+    if not lay or getattr(m.Router, "_layout_forced", False):
+        return
+    layout = int(lay)
+    r_init = m.Router.__init__
+
+    def router_init(self, *a, **k):
+        r_init(self, *a, **k)
+        self.set_layout(layout)
+
+    m.Router.__init__ = router_init
+    m.Router._layout_forced = True
+    core = importlib.import_module("statsd-router_amd.core")
+    c_init = core.Core.__init__
+
+    def core_init(self, *a, **k):
+        c_init(self, *a, **k)
+        self.set_layout(layout)
+
+    core.Core.__init__ = core_init
 
 
 @pytest.fixture(scope="session")
@@ -96,6 +124,7 @@ def load_router_fixture(name):
     return {
         "n": d["n_downstreams"], "ds_hosts": d["ds_hosts"], "ds_data_ports": d["ds_data_ports"],
         "ping_prefix": d["ping_prefix"], "hostname": d["hostname"], "data_port": d["data_port"],
+        "log_level": d.get("log_level", 3),
         "events": events,
         "packets": {int(k): [dec(p) for p in v] for k, v in d["packets"].items()},
         "logs": [(lv, dec(t)) for lv, t in d["logs"]],

@@ -74,6 +74,20 @@ class Router:
                     self.lines.append((m.group(1).decode(), m.group(2)))
                 self._cv.notify_all()
 
+    def messages(self) -> list[tuple[str, bytes]]:
+        """Whole log messages: a message whose text holds newlines (TRACE "got packet", a line with its
+        '\n') spans several stdout lines; continuation lines are joined back with b"\n"."""
+        out: list[list] = []
+        with self._cv:
+            raw = list(self.raw)
+        for line in raw:
+            m = LOG_RE.match(line)
+            if m:
+                out.append([m.group(1).decode(), m.group(2)])
+            elif out:
+                out[-1][1] += b"\n" + line
+        return [(lv, msg) for lv, msg in out]
+
     def wait_for(self, pred, timeout=20.0) -> bool:
         end = time.monotonic() + timeout
         with self._cv:

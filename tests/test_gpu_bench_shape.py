@@ -1,0 +1,184 @@
+"""GPU: route + MTU packing at exactly the configuration bench.py times.
+
+bench.py's route_pack leg routes 32 distinct 16 MiB batches in one sr_route_device_many launch and
+packs all of them in one sr_pack_packets_many. With eight batches or more the packing deals each
+batch's chunks to one XCD (sr_route.hip, mtu_chunk_slot, padded grid slots) and a full-size C2
+batch has about 65,536 lines per shard: 15 chained 4608-line chunks that mtu_emit's walk follows
+lane by lane. These tests run that launch shape (8, 9 and 32 batches; the bench's own seeds, so
+batch b is bench.py's batch b of rank 0) and compare EVERY batch with the oracle: routed records,
+sorted records, packet descriptors, counts and pending bytes out, from random pending bytes in
+(sr-main.c:49-83, push_to_downstream / ds_schedule_flush; the dead-downstream drop of :106).
+The chunk lane layout (route_chunk_kernel) is also forced on a 32-batch launch of C5 batches, the
+shape bench.py captures for C5. Needs an MI355X: `pytest -m gpu`."""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import bench
+from conftest import load_digests
+
+pytestmark = pytest.mark.gpu
+
+_STREAMS: dict = {}
+_ORACLE: dict = {}
+
+
+def _cfg(cfg):
+    desc, batch_bytes, lens, p_inv, shards, seed0, dkey = bench.CONFIGS[cfg]
+    return batch_bytes, lens, p_inv, shards, seed0, dkey
+
+
+def _streams(pkg, cfg, nb):
+    """bench.py's batches 0 .. nb-1 of rank 0 (same generator, same seeds)."""
+    batch_bytes, lens, p_inv, _, seed0, _ = _cfg(cfg)
+    have = _STREAMS.setdefault(cfg, [])
+    while len(have) < nb:
+        b = len(have)
+        have.append(pkg.gen_stream(batch_bytes, lens, seed=seed0 + 65_537 * b, p_invalid=p_inv))
+    return have[:nb]
+
+
+def _alive(cfg, dead):
+    """All alive, or the dead25 mask of tests/golden/digests.json (what bench.py --dead 0.25 uses)."""
+    _, _, _, shards, _, dkey = _cfg(cfg)
+    if not dead:
+        return [1] * shards
+    words = [int(w, 16) for w in load_digests()[f"{dkey}/dead25"]["alive"]]
+    return [(words[k >> 6] >> (k & 63)) & 1 for k in range(shards)]
+
+
+def _oracle_route(oracle, cfg, dead, b, stream, n, alive):
+    key = (cfg, dead, b)
+    if key not in _ORACLE:
+        recs, _, cnt = oracle.route(stream.data, n, alive)
+        _ORACLE[key] = (recs, cnt, oracle.probed_dead(stream.data, n, alive))
+    return _ORACLE[key]
+
+
+def _route_pack_many(pkg, streams, n, alive, fills, layout=None, knobs=()):
+    """One sr_route_device_many launch over every batch (probed-dead bitmaps asked for, as the router
+    and bench.py do), then ONE sr_pack_packets_many over all of them, each from its own fills."""
+    import torch
+
+    nb = len(streams)
+    size = max(int(s.data.size) for s in streams)
+    cap = max(s.n_lines for s in streams)
+    mp = pkg.max_packets(size, n)
+    d_in = torch.zeros((nb, size), dtype=torch.uint8, device="cuda")
+    for b, s in enumerate(streams):
+        d_in[b, : s.data.size].copy_(torch.from_numpy(s.data))
+    d_rec = torch.zeros((nb, cap), dtype=torch.int64, device="cuda")
+    d_cnt = torch.zeros(nb, dtype=torch.int64, device="cuda")
+    d_pd = torch.zeros((nb, max((n + 63) // 64, 1)), dtype=torch.int64, device="cuda")
+    d_srt = torch.zeros((nb, cap), dtype=torch.int64, device="cuda")
+    d_pk = torch.zeros((nb, mp * 2), dtype=torch.int64, device="cuda")
+    d_counts = torch.zeros((nb, 3), dtype=torch.int64, device="cuda")
+    d_fin = torch.from_numpy(np.ascontiguousarray(fills, dtype=np.uint16).view(np.int16)).cuda()
+    d_fout = torch.full((nb, n), -1, dtype=torch.int16, device="cuda")
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream), pkg.Router(n, size) as r:
+        r.set_alive(alive)
+        r.set_stream(stream.cuda_stream)
+        if layout is not None:
+            r.set_layout(layout)
+        for k, v in knobs:
+            r.set_knob(k, v)
+        r.route_device_many([(d_in[b].data_ptr(), int(s.data.size), d_rec[b].data_ptr(), cap, None,
+                              d_cnt[b].data_ptr(), d_pd[b].data_ptr()) for b, s in enumerate(streams)])
+        used_layout = r.last_layout()
+        r.pack_packets_many([(d_rec[b].data_ptr(), d_cnt[b].data_ptr(), cap, d_fin[b].data_ptr(), d_pd[b].data_ptr(),
+                              d_srt[b].data_ptr(), d_pk[b].data_ptr(), mp, d_counts[b].data_ptr(),
+                              d_fout[b].data_ptr()) for b in range(nb)])
+        stream.synchronize()
+    out = []
+    counts = d_counts.cpu().numpy()
+    for b in range(nb):
+        n_lines = int(d_cnt[b].item())
+        np_, nv, nl = (int(x) for x in counts[b])
+        out.append({
+            "n_lines": n_lines,
+            "recs": np.frombuffer(d_rec[b].cpu().numpy().tobytes(), dtype=pkg.RECORD_DTYPE)[:n_lines],
+            "probed": pkg.bitmap_shards(np.frombuffer(d_pd[b].cpu().numpy().tobytes(), dtype=np.uint64), n),
+            "counts": (np_, nv, nl),
+            "sorted": np.frombuffer(d_srt[b].cpu().numpy().tobytes(), dtype=pkg.RECORD_DTYPE)[:nl],
+            "packets": np.frombuffer(d_pk[b].cpu().numpy().tobytes(), dtype=pkg.PACKET_DTYPE)[:np_],
+            "fill_out": d_fout[b].cpu().numpy().view(np.uint16).copy(),
+        })
+    return out, used_layout
+
+
+CASES = [
+    # (config, a quarter of the shards dead, batches in the launch, pending bytes in)
+    ("c2", False, 8, "random"),
+    ("c2", False, 9, "random"),
+    ("c2", False, 32, "random"),
+    ("c2", False, 32, "zero"),      # bench.py's route_pack leg exactly
+    ("c2", True, 32, "random"),
+    ("c3", True, 32, "random"),
+    ("c4", True, 32, "random"),
+    ("c5", False, 32, "random"),
+    ("c5", True, 8, "random"),
+    ("c5", True, 9, "random"),
+    ("c5", True, 32, "random"),
+]
+
+
+@pytest.mark.parametrize("cfg,dead,nb,fill", CASES)
+def test_route_pack_many_full_size(pkg, oracle, cfg, dead, nb, fill):
+    _, _, _, n, _, _ = _cfg(cfg)
+    alive = _alive(cfg, dead)
+    streams = _streams(pkg, cfg, nb)
+    rng = np.random.default_rng(1000 * nb + n + (7 if dead else 0))
+    fills = rng.integers(0, 1451, (nb, n)) if fill == "random" else np.zeros((nb, n), dtype=np.int64)
+    got, _ = _route_pack_many(pkg, streams, n, alive, fills)
+    for b, s in enumerate(streams):
+        recs, cnt, probed = _oracle_route(oracle, cfg, dead, b, s, n, alive)
+        g = got[b]
+        assert g["n_lines"] == cnt == s.n_lines, b
+        assert np.array_equal(g["recs"], recs), f"batch {b}: routed records differ"
+        assert g["probed"].tolist() == probed.tolist(), f"batch {b}: probed-dead shards differ"
+        srt_o, pk_o, fo_o, nv_o = oracle.pack_packets(recs, n, fills[b], probed)
+        assert g["counts"] == (len(pk_o), nv_o, cnt), (b, g["counts"], (len(pk_o), nv_o, cnt))
+        assert np.array_equal(g["sorted"], srt_o), f"batch {b}: sorted records differ"
+        assert np.array_equal(g["packets"].view(np.uint8), pk_o.view(np.uint8)), f"batch {b}: descriptors differ"
+        assert g["fill_out"].tolist() == fo_o.tolist(), f"batch {b}: pending bytes out differ"
+
+
+@pytest.mark.parametrize("dead", [False, True])
+def test_chunk_layout_32_batch_launch_c5(pkg, oracle, dead):
+    """SR_LAYOUT_CHUNKS forced on one 32-batch launch of full-size C5 batches (bench.py's C5 shape:
+    XCD-local classes, the tail look-back across tiles), every batch against the oracle, then
+    packed in the same sr_pack_packets_many call shape."""
+    n = 64
+    alive = _alive("c5", dead)
+    streams = _streams(pkg, "c5", 32)
+    fills = np.random.default_rng(55 + dead).integers(0, 1451, (32, n))
+    got, layout = _route_pack_many(pkg, streams, n, alive, fills, layout=3)
+    assert layout == 3
+    for b, s in enumerate(streams):
+        recs, cnt, probed = _oracle_route(oracle, "c5", dead, b, s, n, alive)
+        assert got[b]["n_lines"] == cnt, b
+        assert np.array_equal(got[b]["recs"], recs), f"batch {b}: chunk-layout records differ"
+        srt_o, pk_o, fo_o, _ = oracle.pack_packets(recs, n, fills[b], probed)
+        assert np.array_equal(got[b]["packets"].view(np.uint8), pk_o.view(np.uint8)), b
+        assert got[b]["fill_out"].tolist() == fo_o.tolist(), b
+
+
+@pytest.mark.parametrize("cfg,nb", [("c2", 32), ("c5", 32), ("c3", 9), ("c4", 8), ("c2", 3)])
+def test_persist_kernel_launch_shapes(pkg, oracle, cfg, nb):
+    """route_persist_kernel (SR_KNOB_PERSIST 2, every shard alive) on bench.py's launch shapes: every
+    batch's records against the oracle, then packed in the same sr_pack_packets_many."""
+    _, _, _, n, _, _ = _cfg(cfg)
+    alive = [1] * n
+    streams = _streams(pkg, cfg, nb)
+    fills = np.random.default_rng(77 + nb).integers(0, 1451, (nb, n))
+    got, layout = _route_pack_many(pkg, streams, n, alive, fills, knobs=[(pkg.SR_KNOB_PERSIST, 2)])
+    assert layout == 3
+    for b, s in enumerate(streams):
+        recs, cnt, probed = _oracle_route(oracle, cfg, False, b, s, n, alive)
+        assert got[b]["n_lines"] == cnt, b
+        assert np.array_equal(got[b]["recs"], recs), f"batch {b}: persistent-kernel records differ"
+        srt_o, pk_o, fo_o, _ = oracle.pack_packets(recs, n, fills[b], probed)
+        assert np.array_equal(got[b]["packets"].view(np.uint8), pk_o.view(np.uint8)), b
+        assert got[b]["fill_out"].tolist() == fo_o.tolist(), b

@@ -61,7 +61,7 @@ def catalogue(seed=11):
     return dg
 
 
-def run_router(exe, datagrams, n_ds, tmp, threads=1):
+def run_router(exe, datagrams, n_ds, tmp, threads=1, log_level=1, messages=False):
     base = free_ports(4 + 2 * n_ds)
     data_port, ctl, sink_base = base, base + 1, base + 4
     ds = [(sink_base + 2 * i, sink_base + 2 * i + 1) for i in range(n_ds)]
@@ -69,8 +69,8 @@ def run_router(exe, datagrams, n_ds, tmp, threads=1):
     sink = subprocess.Popen([SINK, str(sink_base), str(n_ds), "60", "3.0", dump], stdout=subprocess.PIPE,
                             stderr=subprocess.PIPE)
     assert sink.stderr.readline().strip() == b"ready"
-    r = Router(exe, config_text(data_port, ctl, ds, log_level=1, threads=threads, flush=0.1, health=0.1, ping=1000.0,
-                                prefix=PREFIX), tmp)
+    r = Router(exe, config_text(data_port, ctl, ds, log_level=log_level, threads=threads, flush=0.1, health=0.1,
+                                ping=1000.0, prefix=PREFIX), tmp)
     try:
         for i in range(n_ds):
             assert r.wait_for(lambda lv, m, i=i: m == b"ds_health_read_cb downstream %d is up" % i, 20), r.raw[-20:]
@@ -98,6 +98,8 @@ def run_router(exe, datagrams, n_ds, tmp, threads=1):
             if not line.startswith(PREFIX.encode()):
                 got[d][line + b"\n"] += 1
     data_path = (b"udp_read_cb:", b"process_data_line:", b"find_downstream:")
+    if messages:   # every data-path message (TRACE included), whole
+        return got, [(lv, m) for lv, m in r.messages() if m.startswith(data_path)]
     warns = [m for lv, m in r.lines if lv == "WARN" and m.startswith(data_path)]
     return got, warns
 
@@ -180,3 +182,16 @@ def test_timers_run_while_the_socket_never_drains(tmp_path):
     first, last = data_idx[0], data_idx[-1]
     during = sum(g for d, g in seq[first:last + 1])
     assert during >= 4, f"only {during} ping gauges among {last - first + 1} datagrams of a 3 s blast (ping 0.3 s)"
+
+
+@pytest.mark.skipif(not os.path.exists(REFERENCE), reason="reference executable not built (make -C oracle ref)")
+def test_trace_log_matches_reference_executable(tmp_path):
+    """log_level=0 (the reference's default, sr-init.c:252): the executable prints the reference's
+    TRACE lines (sr-main.c:91,102,174) between its WARN lines, message for message and in order, as
+    the reference executable does for the same datagrams; the packets are unchanged."""
+    dg = catalogue(seed=13)[:260]
+    ours, m1 = run_router(OURS, dg, 3, str(tmp_path), log_level=0, messages=True)
+    ref, m2 = run_router(REFERENCE, dg, 3, str(tmp_path), log_level=0, messages=True)
+    assert ours == ref
+    assert sum(lv == "TRACE" for lv, _ in m2) > 2 * len(dg)
+    assert m1 == m2

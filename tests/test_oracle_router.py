@@ -1,5 +1,5 @@
 """CPU: the pure-Python data-thread restatement (oracle/sr_router_oracle.py) reproduces every
-packet, WARN line and final buffer the compiled reference produced for the scripted sessions in
+packet, log line (WARN, and TRACE at log_level 0) and final buffer the compiled reference produced for the scripted sessions in
 tests/golden/router_*.json (push_to_downstream / flush / dead drop / flush timer / ping)."""
 from __future__ import annotations
 
@@ -13,7 +13,8 @@ def test_router_oracle_matches_reference(name):
     import sr_router_oracle as RO
 
     f = load_router_fixture(name)
-    t = RO.DataThread(f["n"], f["ds_hosts"], f["ds_data_ports"], f["ping_prefix"], f["hostname"], f["data_port"])
+    t = RO.DataThread(f["n"], f["ds_hosts"], f["ds_data_ports"], f["ping_prefix"], f["hostname"], f["data_port"],
+                      log_level=f["log_level"])
     t.run(f["events"])
     assert t.logs == f["logs"]
     assert {k: v for k, v in t.packets.items() if v} == f["packets"]
