@@ -382,8 +382,9 @@ int sr_route_pack_trace(sr_ctx *ctx, int slot, const sr_record **records, const 
  *   SR_KNOB_MTU_XCD       1 (default): batches' packing chunks on one XCD from eight batches up;
  *   SR_KNOB_MTU_WALK      1 (default): the chain walked inside mtu_emit up to 64 shards; 0: mtu_chain;
  *   SR_KNOB_PERSIST       launches with every shard alive run the persistent chunk kernel: 0 never,
- *                         1 in the chunk layout, 2 in every layout.
- * Returns 0 or -EINVAL (unknown knob or value). */
+ *                         1 in the chunk layout, 2 in every layout (developer builds only, measured
+ *                         slower: -ENOTSUP otherwise).
+ * Returns 0, -EINVAL (unknown knob or value) or -ENOTSUP. */
 #define SR_KNOB_LB_SPIN 1
 #define SR_KNOB_DEFER_PICKS 2
 #define SR_KNOB_MTU_CHUNK 3

@@ -8,8 +8,8 @@
 // Why: the one-shot kernels give each 16 KiB tile one workgroup whose loads are in
 // flight only during its first ~2.4 us of an ~8 us life, so 7 workgroups per CU keep ~34 KB in
 // flight per CU: at the ~2.4 us latency of loaded HBM that is ~3.7 TB/s, the measured rate. Here a
-// workgroup owns a fixed share of the launch's tiles (tile w, w + W, w + 2W, ... of its XCD class)
-// and issues tile k+1's bytes by LDS-DMA (buffer_load_dwordx4 ... lds: no VGPRs, counted by vmcnt,
+// workgroup takes its XCD class's tiles in order from a counter (one atomic per tile, fetched a tile
+// ahead; workgroups that start late take fewer) and issues tile k+1's bytes by LDS-DMA (buffer_load_dwordx4 ... lds: no VGPRs, counted by vmcnt,
 // waited for with a counted s_waitcnt at the top of the next iteration) before it routes tile k, so
 // every workgroup has a tile in flight all the time: two 16 KiB images per workgroup, 4 workgroups
 // per CU, 64 KiB in flight per CU.
@@ -42,6 +42,7 @@ struct PersistSmem {
     uint64_t kp_hi[kPowHi];            // K^(64 i) (i < 24) }
     uint64_t kinv[kCinv];              // K^-z
     uint32_t scan_head, scan_pub, scan_total;   // scanner blocks
+    uint32_t take;                     // the tile the workgroup's last atomic took
     static constexpr int kWords = 8192;
 };
 static_assert(sizeof(PersistSmem) <= 40 * 1024, "4 workgroups per CU (160 KiB of LDS)");
@@ -91,18 +92,27 @@ __global__ __launch_bounds__(256, 4) void route_persist_kernel(RouteParams p) {
     const uint32_t g = blockIdx.x - p.nb;
     const uint32_t cls = p.xcd_local ? (g & 7u) : 0u;
     const uint32_t w0 = p.xcd_local ? (g >> 3) : g;   // this workgroup's index among its class's
-    const uint32_t W = p.pworkers;                    // workgroups per class
     uint32_t ntc = 0;                                 // tiles of the class
 #pragma unroll
     for (int k = 0; k < kPerClass; ++k)
         if (p.cls_tab[cls][k] != ~0u) ntc = max(ntc, p.cls_tab[cls][k] >> 6);
+    (void)w0;
     const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (w0 >= ntc) {
+    uint32_t *const ctr = &p.ctl->ptile[cls][0];
+    // the class's tiles in order: one atomic per tile (lane 0 of wave 0), shared through LDS
+    auto take = [&]() -> uint32_t {
+        if (tid == 0) sm.take = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wg_barrier();
+        const uint32_t v = __builtin_amdgcn_readfirstlane(sm.take);
+        return v;
+    };
+    const uint32_t ci0 = take();
+    if (ci0 >= ntc) {
         if (tid == 0) arrive(p, blockIdx.x, ep0);
         return;
     }
     // ---- once per workgroup: the first tile's bytes, then the power tables ----------------------
-    persist_issue(p, sm, cls, w0, 0, wave, lane);
+    persist_issue(p, sm, cls, ci0, 0, wave, lane);
     constexpr int kKpWords = 2 * (kPowLo + kPowHi);
     const uint32_t kw = ((const uint32_t *)p.kpow)[tid < kKpWords ? tid : kKpWords - 1];
     const uint32_t iw = ((const uint32_t *)p.cpow)[tid < 2 * kCinv ? tid : 2 * kCinv - 1];
@@ -113,14 +123,17 @@ __global__ __launch_bounds__(256, 4) void route_persist_kernel(RouteParams p) {
     wg_barrier();
     const int o = tid * 64;   // the lane's chunk: tile bytes [o, o + 64)
 
-    for (uint32_t it = 0, ci = w0;; ++it) {
+    uint32_t nci = take();   // the next tile
+    for (uint32_t it = 0, ci = ci0;; ++it) {
         const uint32_t par = it & 1u;
-        const uint32_t nci = ci + W;
         const bool more = nci < ntc;
-        // the next tile's bytes go out before anything of this one is waited for
-        if (more) persist_issue(p, sm, cls, nci, par ^ 1u, wave, lane);
+        // the next tile's bytes go out before anything of this one is waited for, then the atomic
+        // that takes the tile after it (its value is first needed at this iteration's end)
+        uint32_t after = ntc;
         if (more) {
-            if (wave == 0) __builtin_amdgcn_s_waitcnt(0x0F75);   // vmcnt(5): this tile's 5 are in
+            persist_issue(p, sm, cls, nci, par ^ 1u, wave, lane);
+            if (tid == 0) after = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (wave == 0) __builtin_amdgcn_s_waitcnt(0x0F76);   // vmcnt(6): this tile's 5 are in
             else __builtin_amdgcn_s_waitcnt(0x0F74);             // vmcnt(4)
         } else {
             __builtin_amdgcn_s_waitcnt(0x0F70);                  // vmcnt(0)
@@ -413,7 +426,10 @@ __global__ __launch_bounds__(256, 4) void route_persist_kernel(RouteParams p) {
             }
         }
         if (!more) break;
+        if (tid == 0) sm.take = after;
+        wg_barrier();
         ci = nci;
+        nci = __builtin_amdgcn_readfirstlane(sm.take);
     }
     if (tid == 0) arrive(p, blockIdx.x, ep0);
 }

@@ -12,7 +12,10 @@
 #include <utility>
 #include <vector>
 
+#include "chunk_kernel.hpp"
+#ifdef SR_PERSIST_KERNEL   // developer builds only (`make VARIANTS=1`): measured slower, DESIGN.md §9
 #include "persist_kernel.hpp"
+#endif
 
 namespace srk {
 
@@ -435,6 +438,7 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
         }
     }
     if (ds.wide() && hipMemsetAsync(&ds.d_ctl->pending, 0, sizeof(uint32_t), stream) != hipSuccess) return -EIO;
+#ifdef SR_PERSIST_KERNEL
     if constexpr ((ABL & KV_PERSIST) != 0) {
         // one workgroup per resident slot (4 per CU), the scanners' slots included: per XCD class the
         // slots of its XCD less the scanners placed there (block b runs on XCD b % 8)
@@ -459,7 +463,9 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
         }
         p.total_blocks = p.nb + workers;
         hipLaunchKernelGGL((route_persist_kernel<ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
-    } else if constexpr ((ABL & KV_CHUNKS) != 0) {
+    } else
+#endif
+    if constexpr ((ABL & KV_CHUNKS) != 0) {
         static_assert(BLOCK == 256, "route_chunk_kernel: 256 lanes of 64 bytes per 16 KiB tile");
         // its probe stops after the first picks: with two or more dead shards it needs the deferral
         // (no scratch for it, e.g. inside a stream capture: the uniform kernel probes in full)

@@ -145,6 +145,8 @@ struct Control {
     uint32_t layout[8][32];  // KV_SEGMENTS launches, sharded: [0] tiles that weighed the segment
                              // layout, [1] tiles it saves two or more rounds (published per launch
                              // by the last block)
+    uint32_t ptile[8][32];   // route_persist_kernel: per XCD class, the next tile to take (reset by
+                             // the last block)
 };
 
 // One batch of a launch. A launch routes up to kMaxBatches independent batches: tiles
@@ -1204,6 +1206,7 @@ __device__ void arrive(const RouteParams &p, uint32_t blk, uint32_t epoch) {
         __hip_atomic_store(&p.ctl->done[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         weighed += __hip_atomic_exchange(&p.ctl->layout[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         segmented += __hip_atomic_exchange(&p.ctl->layout[s8][1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&p.ctl->ptile[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (weighed && p.layout_out) {   // the host's layout choice reads these (route_host.hpp)
         __hip_atomic_store(&p.layout_out[1], weighed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

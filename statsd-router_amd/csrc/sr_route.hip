@@ -88,11 +88,13 @@ static void free_ptr(void *p) { (void)hipFree(p); }
 // never the shipped library): SR_VARIANT in the environment then selects one.
 static int launch_product(DeviceState &ds, const RouteParams &p, hipStream_t stream) {
     const bool seg = ds.choose_segments(stream);
-    // every shard alive, persistent chunk kernel asked for (SR_KNOB_PERSIST)
+#ifdef SR_PERSIST_KERNEL
+    // every shard alive, persistent chunk kernel asked for (SR_KNOB_PERSIST; developer builds)
     if (ds.dead == 0 && ds.persist && !seg && (ds.persist == 2 || ds.last_layout == SR_LAYOUT_CHUNKS)) {
         ds.last_layout = SR_LAYOUT_CHUNKS;
         return launch_route<kBlock, KV_CHUNKS | KV_ALIVE | KV_PERSIST>(ds, p, stream);
     }
+#endif
     if (ds.last_layout == SR_LAYOUT_CHUNKS) {
         if (ds.dead == 0) return launch_route<kBlock, KV_CHUNKS | KV_ALIVE | SR_CHUNK_ABL>(ds, p, stream);
         return launch_route<kBlock, KV_CHUNKS | SR_CHUNK_ABL>(ds, p, stream);
@@ -263,9 +265,13 @@ int sr_set_knob(sr_ctx *c, int knob, int64_t v) {
         c->mtu_chunk = (uint32_t)v;
         return 0;
     case SR_KNOB_PERSIST:
+#ifdef SR_PERSIST_KERNEL
         if (v < 0 || v > 2) return -EINVAL;
         c->ds.persist = (uint32_t)v;
         return 0;
+#else
+        return v == 0 ? 0 : -ENOTSUP;   // the kernel is in developer builds only (`make VARIANTS=1`)
+#endif
     case SR_KNOB_MTU_XCD:
     case SR_KNOB_MTU_WALK:
         if (v != 0 && v != 1) return -EINVAL;

@@ -156,6 +156,15 @@ def test_chunks_tile_straddles_and_lookback(pkg, oracle, spin):
 PERSIST = 2   # SR_KNOB_PERSIST: every all-alive launch on route_persist_kernel
 
 
+def _persist_or_skip(pkg, r):
+    """route_persist_kernel is built into developer libraries only (make VARIANTS=1, SR_ROUTE_LIB)."""
+    try:
+        r.set_knob(pkg.SR_KNOB_PERSIST, PERSIST)
+    except pkg.SrError as e:
+        r.close()
+        pytest.skip(f"route_persist_kernel not in this build ({e})")
+
+
 @pytest.mark.parametrize("n", [4, 64, 7])
 @pytest.mark.parametrize("spin", [None, 0])
 def test_persist_kernel_matches_oracle(pkg, oracle, n, spin):
@@ -164,12 +173,12 @@ def test_persist_kernel_matches_oracle(pkg, oracle, n, spin):
     rng = np.random.default_rng(21)
     r = pkg.Router(n, 4 << 20)
     try:
-        r.set_knob(pkg.SR_KNOB_PERSIST, PERSIST)
+        _persist_or_skip(pkg, r)
         if spin is not None:
             r.set_knob(pkg.SR_KNOB_LB_SPIN, spin)
         for name, data in list(_streams(pkg)) + [("straddles", _tile_straddles(rng))]:
             _assert_same(r.route(data, want_hashes=True), oracle.route(data, n, None), f"{name} persist N={n} spin={spin}")
-            assert r.last_layout() == CHUNKS
+            assert r.last_layout() in (CHUNKS, SEGMENTS)   # (AUTO's first launch is a segment probe)
     finally:
         r.close()
 
@@ -182,7 +191,7 @@ def test_persist_full_size_digests(pkg):
         s = pkg.gen_stream(d["nbytes"], d["line_lens"], seed=d["seed"], p_invalid=d["p_invalid"])
         r = pkg.Router(d["n_downstreams"], d["nbytes"])
         try:
-            r.set_knob(pkg.SR_KNOB_PERSIST, PERSIST)
+            _persist_or_skip(pkg, r)
             recs, hs, cnt = r.route(s.data, want_hashes=True)
         finally:
             r.close()
