@@ -191,6 +191,10 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     constexpr int kKpWords = 2 * (kPowLo + kPowHi);
     const uint32_t kw = ((const uint32_t *)p.kpow)[tid < kKpWords ? tid : kKpWords - 1];
     const uint32_t iw = ((const uint32_t *)p.cpow)[tid < 2 * kCinv ? tid : 2 * kCinv - 1];
+    // the block scan's per-lane constants K^(64 (255 - l)) and K^-(64 (255 - l)), queued behind the
+    // tile's loads: in a tile that some line crosses a chunk boundary of (most C5 tiles), asked for
+    // only after the first barrier they were a dependent round trip of their own
+    const uint64_t R = p.cpow[kCinv + tid], RI = p.cpow[kCinv + 256 + tid];
     if (T0 + 16384u > nbytes) {
         // the batch's last tile: a piece past the end reads as zeros, but the range check of a 16-byte
         // load that straddles the end is not byte-exact (its bytes before the end can read as zero
@@ -331,7 +335,6 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     // ---- Y and the slots (only when some line crosses a chunk boundary) ------------------------
     uint64_t Y = tid == 0 ? U : 0ull;   // exact for chunk 0; elsewhere it cancels when s, c share a chunk
     if (long_tile) {
-        const uint64_t R = p.cpow[kCinv + tid], RI = p.cpow[kCinv + 256 + tid];
         const uint64_t Sw = wave_scan64(U * R, 0ull, [](uint64_t l, uint64_t r) { return l + r; });
         if (lane == 63) sm.wv[wave] = Sw;
         wg_barrier();   // B2
