@@ -689,21 +689,20 @@ def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, de
                                         self.h[b].data_ptr() if dead else None, self.cnt[b].data_ptr(),
                                         self.pd[b].data_ptr()) for b in range(M)])
 
-        def pack(self):   # the batches of M data threads: independent pending bytes, one set of launches
-            self.rt.pack_packets_many([(self.rec[b].data_ptr(), self.cnt[b].data_ptr(), max_lines,
-                                        self.fill[b].data_ptr(), self.pd[b].data_ptr(), self.srt[b].data_ptr(),
-                                        self.pk[b].data_ptr(), mp, self.counts[b].data_ptr(),
-                                        self.fout[b].data_ptr()) for b in range(M)])
+        def route_pack(self):   # sr_route_pack_many: the route kernel's tile histograms feed the sort
+            self.rt.route_pack_many([(base + (self.first + b) * batch_bytes, sizes[self.first + b],
+                                      self.rec[b].data_ptr(), max_lines, self.h[b].data_ptr() if dead else None,
+                                      self.cnt[b].data_ptr(), self.pd[b].data_ptr(), self.fill[b].data_ptr(),
+                                      self.srt[b].data_ptr(), self.pk[b].data_ptr(), mp, self.counts[b].data_ptr(),
+                                      self.fout[b].data_ptr()) for b in range(M)])
 
         def capture(self):
             with torch.cuda.stream(self.st):
-                self.route()
-                self.pack()                                  # eager once: the packing scratch is allocated here
+                self.route_pack()                            # eager once: the packing scratch is allocated here
                 self.st.synchronize()
                 self.g_all, self.g_route = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
                 with torch.cuda.graph(self.g_all, stream=self.st):
-                    self.route()
-                    self.pack()
+                    self.route_pack()
                 with torch.cuda.graph(self.g_route, stream=self.st):
                     self.route()
 
@@ -743,9 +742,10 @@ def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, de
            "packets_per_launch": packets,
            "probed_dead_shards": int(sum(bin(int(w) & (2**64 - 1)).count("1") for w in t1.pd[0].tolist())),
            "verify": verify,
-           "note": (f"one route launch over {M} batches with their probed-dead bitmaps (sr-main.c:106) + one "
-                    f"sr_pack_packets_many over them (regroup by downstream, next-fit 1450-byte packets), one "
-                    f"graph, {reps} replays")}
+           "note": (f"sr_route_pack_many: one route launch over {M} batches with their probed-dead bitmaps "
+                    f"(sr-main.c:106; all alive with <= 16 shards: also each tile's per-shard line counts) + the "
+                    f"packing of all of them (regroup by downstream, next-fit 1450-byte packets), one graph, {reps} "
+                    f"replays; packing_ms = that graph - the route launch's graph")}
     if threads < 2:
         return out
     # two data threads on one GPU: a second context on its own stream over the next M batches

@@ -326,6 +326,14 @@ typedef struct sr_pack_batch {
 } sr_pack_batch;
 int sr_pack_packets_many(sr_ctx *ctx, const sr_pack_batch *batches, size_t count);
 
+/* Route and pack device-resident batches in one call: sr_route_device_many over `route` (one launch)
+ * followed by sr_pack_packets_many over `pack`, whose batch i must read what route batch i writes
+ * (pack[i].d_recs == route[i].d_out, same d_n_records, max_records and d_probed_dead; -EINVAL
+ * otherwise). Identical outputs; with every shard alive and at most 16 downstreams the route kernel
+ * also hands each 16 KiB tile's per-downstream line counts to the packing, which then sorts the
+ * records without a counting pass of its own over them. count <= SR_MAX_BATCHES_PER_LAUNCH. */
+int sr_route_pack_many(sr_ctx *ctx, const sr_batch *route, const sr_pack_batch *pack, size_t count);
+
 /* Host-memory batch, routed and packed in one call (what a data thread's read callback needs):
  * `fill` (n_downstreams u16) is the pending bytes per downstream before the batch and receives the
  * pending bytes after it; `sorted` (max_records) the regrouped records; `packets` (max_packets) the
@@ -383,7 +391,9 @@ int sr_route_pack_trace(sr_ctx *ctx, int slot, const sr_record **records, const 
  *   SR_KNOB_MTU_WALK      1 (default): the chain walked inside mtu_emit up to 64 shards; 0: mtu_chain;
  *   SR_KNOB_PERSIST       launches with every shard alive run the persistent chunk kernel: 0 never,
  *                         1 in the chunk layout, 2 in every layout (developer builds only, measured
- *                         slower: -ENOTSUP otherwise).
+ *                         slower: -ENOTSUP otherwise);
+ *   SR_KNOB_HIST          1 (default): sr_route_pack_many / sr_route_pack_* hand the route kernel's tile
+ *                         histograms to the packing; 0: the packing counts the records itself.
  * Returns 0, -EINVAL (unknown knob or value) or -ENOTSUP. */
 #define SR_KNOB_LB_SPIN 1
 #define SR_KNOB_DEFER_PICKS 2
@@ -391,6 +401,7 @@ int sr_route_pack_trace(sr_ctx *ctx, int slot, const sr_record **records, const 
 #define SR_KNOB_MTU_XCD 4
 #define SR_KNOB_MTU_WALK 5
 #define SR_KNOB_PERSIST 6
+#define SR_KNOB_HIST 7
 int sr_set_knob(sr_ctx *ctx, int knob, int64_t value);
 
 /* Page-locked host memory for the batches and outputs of the host-memory calls (their copies then

@@ -52,13 +52,14 @@ ABI_FUNCTIONS = (
     "sr_pack_many_by_owner", "sr_pack_packets", "sr_pack_packets_many", "sr_route_pack_batch", "sr_alloc_host", "sr_free_host", "sr_sync", "sr_close", "sr_version",
     "sr_comm_id", "sr_comm_open", "sr_comm_close", "sr_exchange_sizes", "sr_exchange_data",
     "sr_exchange_plan", "sr_exchange_run", "sr_exchange_rebase", "sr_route_pack_submit", "sr_route_pack_result",
-    "sr_set_trace", "sr_route_pack_trace", "sr_set_knob",
+    "sr_set_trace", "sr_route_pack_trace", "sr_set_knob", "sr_route_pack_many",
 )
 SR_MAX_PACK_DOWNSTREAMS = 4096
 SR_LAYOUT_AUTO, SR_LAYOUT_UNIFORM, SR_LAYOUT_SEGMENTS, SR_LAYOUT_CHUNKS = 0, 1, 2, 3
 SR_COMM_ID_BYTES = 128
 # sr_set_knob (developer / test knobs of one context; none changes a result)
 SR_KNOB_LB_SPIN, SR_KNOB_DEFER_PICKS, SR_KNOB_MTU_CHUNK, SR_KNOB_MTU_XCD, SR_KNOB_MTU_WALK, SR_KNOB_PERSIST = 1, 2, 3, 4, 5, 6
+SR_KNOB_HIST = 7
 LAYOUT_NAMES = {0: "none", 1: "uniform", 2: "segments", 3: "chunks"}
 PACKET_DTYPE = np.dtype([("first", "<u4"), ("nlines", "<u2"), ("shard", "<u2"), ("length", "<u2"),
                          ("carry", "<u2"), ("open", "<u4")])
@@ -200,8 +201,11 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_set_trace": (ctypes.c_int, [vp, ctypes.c_int]),
         "sr_route_pack_trace": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), c_size_p]),
         "sr_set_knob": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int64]),
+        "sr_route_pack_many": (ctypes.c_int, [vp, ctypes.POINTER(SrBatch), ctypes.POINTER(SrPackBatch), ctypes.c_size_t]),
     }
     for name in ABI_FUNCTIONS:
+        if os.environ.get("SR_ROUTE_LIB") and not hasattr(lib, name):
+            continue   # an older build under A/B (SR_ROUTE_LIB) may lack entry points added since
         fn = getattr(lib, name)  # raises AttributeError if the export is missing
         fn.restype, fn.argtypes = sig[name]
     return lib
@@ -494,6 +498,18 @@ class Router:
         for i, b in enumerate(batches):
             arr[i] = SrPackBatch(*[x or None if j not in (2, 7) else x for j, x in enumerate(b)])
         _check(self._lib.sr_pack_packets_many(self._h, arr, len(batches)), "sr_pack_packets_many")
+
+    def route_pack_many(self, batches) -> None:
+        """sr_route_pack_many: batches = [(d_bytes, nbytes, d_out, max_records, d_hashes, d_n_records,
+        d_probed_dead, d_fill_in, d_sorted, d_packets, max_packets, d_counts, d_fill_out), ...]: each routed
+        into d_out, then packed from it (raw device pointers, 0 = NULL)."""
+        n = max(len(batches), 1)
+        ra, pa = (SrBatch * n)(), (SrPackBatch * n)()
+        for i, b in enumerate(batches):
+            db, nb, do, mr, dh, dc, dp, fi, ds, dpk, mp, dcnt, fo = b
+            ra[i] = SrBatch(db, nb, do, mr, dh or None, dc, dp or None)
+            pa[i] = SrPackBatch(do, dc, mr, fi or None, dp or None, ds, dpk, mp, dcnt, fo)
+        _check(self._lib.sr_route_pack_many(self._h, ra, pa, len(batches)), "sr_route_pack_many")
 
     def exchange_sizes(self, comm: "Comm", d_owner_counts: int, d_recv_counts: int):
         """sr_exchange_sizes: returns (sent, received) as u64 [world, 2] {lines, bytes} arrays."""

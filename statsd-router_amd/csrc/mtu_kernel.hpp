@@ -95,6 +95,7 @@ struct MtuBatchArg {
     uint32_t max_packets;
     uint32_t tile0;                // first record tile of the batch in the launch's scratch
     uint32_t chunk0;               // first chunk of the batch in the launch's scratch
+    uint32_t grp0;                 // group mode: the batch's first scatter group in the launch
 };
 
 struct MtuLaunch {
@@ -113,6 +114,10 @@ struct MtuLaunch {
     uint32_t *gp0;                     // [chunks][kMtuP0 + 1] the first prefix sums and the chunk's bytes
     uint64_t *dbg;                     // SR_MTU_STAMPS developer builds only: 8 timestamps per chunk
     uint32_t xcd;                      // chunk kernels: every batch's chunks on one XCD (mtu_chunk_slot)
+    // group mode (sr_route_pack_many): the sort's tiles are the route kernel's 16 KiB tiles, whose key
+    // histograms it wrote (RouteParams::hist, = tile_counts); the scatter's wave takes `group` of
+    // them (0: the classic 1024-record tiles of mtu_count)
+    uint32_t group, groups;
     MtuBatchArg b[kMtuMaxBatches];
 };
 static_assert(sizeof(MtuLaunch) < 3584, "kernel argument size");
@@ -230,7 +235,7 @@ __device__ __forceinline__ void mtu_stamp(const MtuLaunch &L, uint32_t gc, int s
 // than one round trip per 64 records; the caller ignores positions past the batch, n > r0 >= 0).
 constexpr int kMtuPerLane = kMtuTile / 64;
 __device__ __forceinline__ void mtu_load_tile(const MtuParams &p, uint32_t r0, uint32_t n, int lane,
-                                              sr_record (&r)[kMtuPerLane]) {
+                                              sr_record (&r)[kMtuPerLane]) {   // records [r0, n) (n > r0)
 #pragma unroll
     for (int k = 0; k < kMtuPerLane; ++k) {   // clamped, unconditional: the eight loads in flight together
         const uint32_t i = r0 + (uint32_t)(64 * k + lane);
@@ -392,6 +397,67 @@ void mtu_scatter_kernel(MtuLaunch L) {
             if (!(same & lt)) pos[key] = base + (uint32_t)__popcll(same);   // the key's first lane
         }
         mtu_wave_sync();
+    }
+}
+
+// Group mode (sr_route_pack_many): wave g sorts the records of route tiles [q G, q G + G) of its
+// batch, whose per-key histograms the route kernel published and mtu_scan turned into positions
+// (pos[k][t] = the sorted position of tile t's first key-k record). The tiles' records are one
+// input range [R(t0), R(t1)) with R(t) = sum over keys of pos[k][t] - pos[k][0], and for every key
+// the group's records follow each other in the sorted order from pos[k][t0]: the classic scatter over
+// that range in rounds of kMtuTile records, no count pass over the records before it.
+__global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_scatter_groups_kernel(MtuLaunch L) {
+    extern __shared__ uint32_t lds_pos[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t g = blockIdx.x * kMtuSortWaves + (uint32_t)wave;
+    if (g >= L.groups) return;
+    const uint32_t bi = mtu_batch_of(L, g, [](const MtuBatchArg &a) { return a.grp0; });
+    const MtuParams p = mtu_view(L, bi);
+    const uint32_t nk = p.nds + 1, q = g - L.b[bi].grp0, nt = p.ntiles;
+    const uint32_t t0 = q * L.group, t1 = min(t0 + L.group, nt);
+    uint32_t *pos = lds_pos + (size_t)wave * nk;
+    const uint32_t n = mtu_lines(p);
+    if (t0 >= nt) return;
+    uint32_t a0 = 0, a1 = 0;
+    for (uint32_t k = (uint32_t)lane; k < nk; k += 64) {
+        const uint32_t *col = p.tile_counts + (size_t)k * nt;
+        const uint32_t b0 = col[0], v0 = col[t0];
+        pos[k] = v0;
+        a0 += v0 - b0;
+        a1 += (t1 < nt ? col[t1] : col[0]) - b0;
+    }
+    const uint32_t r0 = wave_add32(a0);
+    const uint32_t r1 = t1 < nt ? wave_add32(a1) : n;
+    mtu_wave_sync();
+    const uint64_t lt = (1ull << lane) - 1ull;
+    const uint32_t kbits = nk > 1 ? 32u - (uint32_t)__clz(nk - 1u) : 0u;
+    for (uint32_t rb = r0; rb < r1; rb += kMtuTile) {
+        const uint32_t re = min(rb + (uint32_t)kMtuTile, r1);
+        sr_record rr[kMtuPerLane];
+        mtu_load_tile(p, rb, re, lane, rr);
+        uint32_t keys[kMtuPerLane];
+#pragma unroll
+        for (int ck = 0; ck < kMtuPerLane; ++ck) keys[ck] = mtu_key(rr[ck], p.nds);
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the round's records are in registers
+#pragma unroll
+        for (int ck = 0; ck < kMtuPerLane; ++ck) {
+            const uint32_t i = rb + (uint32_t)(64 * ck + lane);
+            const bool valid = i < re;
+            const uint32_t key = keys[ck];
+            uint64_t same = __ballot(valid);
+            for (uint32_t b = 0; b < kbits; ++b) {
+                const bool bit = ((key >> b) & 1u) != 0;
+                const uint64_t bm = __ballot(bit);
+                same &= bit ? bm : ~bm;
+            }
+            const uint32_t base = pos[key];
+            mtu_wave_sync();   // every lane's read before a leader's write
+            if (valid) {
+                p.sorted[base + (uint32_t)__popcll(same & lt)] = rr[ck];
+                if (!(same & lt)) pos[key] = base + (uint32_t)__popcll(same);
+            }
+            mtu_wave_sync();
+        }
     }
 }
 

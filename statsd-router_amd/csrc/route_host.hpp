@@ -101,6 +101,8 @@ struct DeviceState {
     // SR_KNOB_PERSIST: all-alive launches in the chunk layout (1), or in any layout (2), run the
     // persistent kernel (route_persist_kernel); 0: never
     uint32_t persist = 0;
+    uint32_t *d_hist = nullptr;      // RouteParams::hist (sr_route_pack_many), max_tiles x kHistKeys
+    bool last_hist = false;          // the last launch wrote its tiles' key histograms
     uint32_t persist_slots = 0;      // resident route_persist_kernel workgroups on the device (0: not yet asked)
 
     int init(size_t max_batch_bytes, uint32_t n_downstreams) {
@@ -178,6 +180,8 @@ struct DeviceState {
         (void)hipFree(d_pending);
         (void)hipFree(d_defer);
         (void)hipFree(d_tile_pd);
+        (void)hipFree(d_hist);
+        d_hist = nullptr;
         d_defer = nullptr;
         d_tile_pd = nullptr;
         defer_cap = 0;
@@ -483,6 +487,8 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
         hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     }
     if (hipGetLastError() != hipSuccess) return -EIO;
+    // the key histograms exist only where route_kernel counted them (every shard alive)
+    ds.last_hist = p.hist && (ABL & KV_ALIVE) && !(ABL & KV_CHUNKS);
     if (p.defer || p.mark) {   // the probes past their first two picks and the OR of the tiles' probed-dead
                                // slots (probe_defer_kernel), grid y = batch
         // blocks past a batch's record count return at once; the rest loop over chunks of 4 waves

@@ -153,6 +153,7 @@ struct Control {
 // [tile0, tile0 + ntiles) of the grid belong to batch i, each batch with its own look-back chain
 // (status granules at the same grid indices) and its own records and line count.
 constexpr int kMaxBatches = 32;
+constexpr int kHistKeys = 17;  // RouteParams::hist: up to 16 shards + the unrouted key
 constexpr int kPerClass = 8;   // batches per XCD class: <= 4 with 8+ batches (XCD-local), <= 7 below
 struct BatchDesc {
     const uint8_t *bytes;
@@ -202,6 +203,10 @@ struct RouteParams {
     uint64_t *tail;
     uint32_t lb_spin;
     uint32_t pworkers;       // route_persist_kernel: workgroups per XCD class (persist_kernel.hpp)
+    // route + pack launches (sr_route_pack_many; every shard alive, at most kHistKeys - 1 shards): per
+    // tile its records' key histogram (shard, or nds = unrouted), key-major per batch at
+    // hist[(nds + 1) * sbase + key * ntiles + t], for the packing's sort (mtu_kernel.hpp); null: off
+    uint32_t *hist;
     // per XCD class c, its batches in tile order: (class-local end tile << 6) | batch index;
     // ~0u after the last (one scalar load finds a tile's batch)
     uint32_t cls_tab[8][kPerClass];
@@ -752,6 +757,7 @@ struct SmemT {
     uint64_t kp_inv[kPowInv];        // K^-z (an LDS read rather than three 64-bit constants held in VGPRs)
     static constexpr int kPowWords = (kPowLo + kPowHi + kPowInv) * 2;   // u32 words of the three tables
     int32_t s_pre, c_pre;            // straddling line: tile-relative start / first colon before T0
+    uint32_t hist[kHistKeys];        // RouteParams::hist: the tile's records per key
     uint32_t epoch, base;
     uint32_t scan_head, scan_pub, scan_total;   // scanner: bases computed / published, line total
 };
@@ -1570,6 +1576,8 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 }
                 const uint32_t rec = base + (uint32_t)j;
                 if (rec < bd.max_records) {
+                    if constexpr ((ABL & KV_ALIVE) != 0)   // the packing's key histogram (ds_add, no return)
+                        if (p.hist) atomicAdd(&sm.hist[route < p.nds ? route : p.nds], 1u);
                     if (deferred) bd.dhash[rec] = h;
                     if (!(ABL & KV_ALIVE) && route == kRoutePending && !deferred) {
                         const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
@@ -1849,6 +1857,7 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     if (!(ABL & KV_ALIVE) && p.mark && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
         sm.img[(uint32_t)tid * 17 + 16] = 0u;
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
+    if ((ABL & KV_ALIVE) && p.hist && tid < kHistKeys) sm.hist[tid] = 0u;
     uint64_t nlm, clm;
     uint32_t c_in;
     tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
@@ -1860,6 +1869,12 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
             const uint32_t hi = sm.img[(kMarkRow0 + 2 * (uint32_t)tid + 1) * 17 + 16];
             p.tile_pd[(size_t)(p.b[bi].sbase + t) * p.nwords + tid] = ((uint64_t)hi << 32) | lo;
         }
+    }
+    if ((ABL & KV_ALIVE) && p.hist) {   // the tile's key histogram for the packing (sr_route_pack_many)
+        wg_barrier();
+        const BatchDesc &bd = p.b[bi];
+        if ((uint32_t)tid <= p.nds)
+            p.hist[(size_t)(p.nds + 1) * bd.sbase + (size_t)tid * bd.ntiles + t] = sm.hist[tid];
     }
     if (tid == 0) arrive(p, blockIdx.x, ep0);
     stamp<ABL>(p, tid, g, 9);

@@ -57,6 +57,7 @@ struct sr_ctx {
     // packing knobs (sr_set_knob): forced chunk lines (0: by shape), XCD-local chunks, chain walked in emit
     uint32_t mtu_chunk;
     int mtu_xcd, mtu_walk;
+    int hist;                     // SR_KNOB_HIST: route + pack launches hand the tiles' histograms over
     // page-locked, device-mapped outputs of sr_route_pack_submit: slots 0 and 1, slot 2 is
     // sr_route_pack_batch's own
     struct Slot {
@@ -213,6 +214,7 @@ int sr_open(sr_ctx **out, int device, size_t max_batch_bytes, uint32_t n_downstr
     c->device = device;
     c->mtu_xcd = 1;
     c->mtu_walk = 1;
+    c->hist = 1;
     int rc = -ENOMEM;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) goto fail;
     c->stream = c->own_stream;
@@ -274,8 +276,9 @@ int sr_set_knob(sr_ctx *c, int knob, int64_t v) {
 #endif
     case SR_KNOB_MTU_XCD:
     case SR_KNOB_MTU_WALK:
+    case SR_KNOB_HIST:
         if (v != 0 && v != 1) return -EINVAL;
-        (knob == SR_KNOB_MTU_XCD ? c->mtu_xcd : c->mtu_walk) = (int)v;
+        (knob == SR_KNOB_MTU_XCD ? c->mtu_xcd : knob == SR_KNOB_MTU_WALK ? c->mtu_walk : c->hist) = (int)v;
         return 0;
     default:
         return -EINVAL;
@@ -453,7 +456,11 @@ extern "C" size_t sr_mtu_stamps(uint64_t *dst, size_t max_chunks) {
 }
 #endif
 
-int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) {
+// hist (group mode): the key histograms of the route kernel's tiles for these batches, written by the
+// context's last route launch (RouteParams::hist); route_bytes: each batch's bytes in that launch
+// (its tiles: ceil(bytes / 16 KiB), numbered in batch order as launch_route numbers them)
+static int pack_many_impl(sr_ctx *c, const sr_pack_batch *batches, size_t count, uint32_t *hist,
+                          const size_t *route_bytes) {
     if (!c || !batches || count == 0 || count > (size_t)kMtuMaxBatches) return -EINVAL;
     const uint32_t nds = c->ds.nds;
     if (nds > SR_MAX_PACK_DOWNSTREAMS) return -EINVAL;
@@ -467,7 +474,8 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     uint32_t ch = all_records <= (uint64_t)(nds ? nds : 1) * 32u * kMtuChunk ? (uint32_t)kMtuChunkSmall
                                                                             : (uint32_t)kMtuChunk;
     if (c->mtu_chunk) ch = c->mtu_chunk;   // SR_KNOB_MTU_CHUNK (A/B runs)
-    uint32_t tiles = 0, chunks = 0;
+    uint32_t tiles = 0, chunks = 0, groups = 0;
+    constexpr uint32_t kGroup = 4;   // route tiles per scatter wave (C2: 1024 records)
     for (size_t j = 0; j < count; ++j) {
         const sr_pack_batch &b = batches[j];
         if (!b.d_n_records || !b.d_counts || (nds && !b.d_fill_out) || b.max_records > 0xFFFFFFF0ull) return -EINVAL;
@@ -486,19 +494,28 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
         a.max_packets = (uint32_t)(b.max_packets > 0xFFFFFFFFull ? 0xFFFFFFFFull : b.max_packets);
         a.tile0 = tiles;
         a.chunk0 = chunks;
-        const uint64_t nt = (b.max_records + kMtuTile - 1) / kMtuTile;
-        tiles += (uint32_t)(nt ? nt : 1);
+        if (hist) {   // the route launch's tiles of this batch
+            const uint32_t nt = (uint32_t)((route_bytes[j] + 16383) / 16384);
+            a.grp0 = groups;
+            groups += (nt + kGroup - 1) / kGroup;
+            tiles += nt;
+        } else {
+            const uint64_t nt = (b.max_records + kMtuTile - 1) / kMtuTile;
+            tiles += (uint32_t)(nt ? nt : 1);
+        }
         chunks += (uint32_t)((b.max_records + ch - 1) / ch) + nds + 1;
     }
     (void)hipSetDevice(c->device);
-    int rc = mtu_reserve(c, tiles, chunks, (uint32_t)count);
+    int rc = mtu_reserve(c, hist ? 0u : tiles, chunks, (uint32_t)count);
     if (rc) return rc;
     L.nds = nds;
+    L.group = hist ? kGroup : 0u;
+    L.groups = groups;
     L.nb = (uint32_t)count;
     L.tiles = tiles;
     L.chunks = chunks;
     L.chunk_lines = ch;
-    L.tile_counts = c->d_mtu_tiles;
+    L.tile_counts = hist ? hist : c->d_mtu_tiles;
     L.keys = c->d_mtu_keys;
     L.closed = c->d_mtu_keys + (size_t)kMtuMaxBatches * (2 * (size_t)nds + 4);
     L.chunk_shard = c->d_mtu_chunks;
@@ -541,10 +558,18 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     // up to 4 x 4097 counters: past the 64 KiB default
     ensure_dyn_lds((const void *)mtu_count_kernel, 96 * 1024);
     ensure_dyn_lds((const void *)mtu_scatter_kernel, 96 * 1024);
-    const uint32_t sort_blocks = (tiles + kMtuSortWaves - 1) / kMtuSortWaves;
-    hipLaunchKernelGGL(mtu_count_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
-    hipLaunchKernelGGL(mtu_scan_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
-    hipLaunchKernelGGL(mtu_scatter_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
+    if (hist) {   // the route kernel counted the keys: scan its tiles' histograms, scatter by groups of tiles
+        ensure_dyn_lds((const void *)mtu_scatter_groups_kernel, 96 * 1024);
+        const uint32_t gblocks = (groups + kMtuSortWaves - 1) / kMtuSortWaves;
+        hipLaunchKernelGGL(mtu_scan_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
+        if (gblocks)
+            hipLaunchKernelGGL(mtu_scatter_groups_kernel, dim3(gblocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
+    } else {
+        const uint32_t sort_blocks = (tiles + kMtuSortWaves - 1) / kMtuSortWaves;
+        hipLaunchKernelGGL(mtu_count_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
+        hipLaunchKernelGGL(mtu_scan_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
+        hipLaunchKernelGGL(mtu_scatter_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
+    }
     if (ch == (uint32_t)kMtuChunk)
         hipLaunchKernelGGL(mtu_table_kernel<kMtuChunk>, dim3(chunk_grid), dim3(kMtuTableBlock), 0, c->stream, L);
     else
@@ -567,6 +592,49 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
         else hipLaunchKernelGGL((mtu_emit_kernel<kMtuChunkSmall, false>), dim3(chunk_grid), dim3(kMtuBlock), 0, c->stream, L);
     }
     return hipGetLastError() == hipSuccess ? 0 : -EIO;
+}
+
+int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) {
+    return pack_many_impl(c, batches, count, nullptr, nullptr);
+}
+
+// Route (one launch) and pack. With every shard alive and at most kHistKeys - 1 shards the route
+// kernel (uniform / segment layouts) also writes each tile's key histogram and the packing skips
+// mtu_count, its own pass over the records.
+static int route_pack_impl(sr_ctx *c, const sr_batch *route, const sr_pack_batch *pack, size_t count) {
+    DeviceState &ds = c->ds;
+    const bool want = c->hist && ds.dead == 0 && ds.nds >= 1 && ds.nds < (uint32_t)kHistKeys;
+    if (want && !ds.d_hist) {
+        const size_t words = (size_t)(ds.max_tiles ? ds.max_tiles : 1) * kHistKeys;
+        if (hipMalloc(&ds.d_hist, words * sizeof(uint32_t)) != hipSuccess) ds.d_hist = nullptr;
+    }
+    RouteParams p = ds.params();
+    size_t bytes[kMaxBatches];
+    for (size_t i = 0; i < count; ++i) {
+        DeviceState::add_batch(p, route[i].d_bytes, route[i].nbytes, route[i].d_out, route[i].max_records,
+                               route[i].d_hashes, route[i].d_n_records, route[i].d_probed_dead);
+        bytes[i] = route[i].nbytes;
+    }
+    p.hist = want ? ds.d_hist : nullptr;
+    ds.last_hist = false;
+    int rc = launch_variant(ds, p, c->stream);
+    if (rc) return rc;
+    return pack_many_impl(c, pack, count, ds.last_hist ? ds.d_hist : nullptr, bytes);
+}
+
+int sr_route_pack_many(sr_ctx *c, const sr_batch *route, const sr_pack_batch *pack, size_t count) {
+    if (!c || !route || !pack || count == 0 || count > (size_t)kMaxBatches) return -EINVAL;
+    for (size_t i = 0; i < count; ++i) {
+        const sr_batch &b = route[i];
+        if (!b.d_n_records || (b.nbytes && !b.d_bytes) || b.nbytes > c->ds.max_batch) return -EINVAL;
+        if (b.max_records && !b.d_out) return -EINVAL;
+        // the packing reads what the route writes
+        if (pack[i].d_recs != b.d_out || pack[i].d_n_records != b.d_n_records || pack[i].max_records != b.max_records ||
+            pack[i].d_probed_dead != b.d_probed_dead)
+            return -EINVAL;
+    }
+    (void)hipSetDevice(c->device);
+    return route_pack_impl(c, route, pack, count);
 }
 
 int sr_pack_packets(sr_ctx *c, const sr_record *d_recs, const uint64_t *d_n_records, size_t max_records,
@@ -696,12 +764,10 @@ static int pack_submit(sr_ctx *c, int k, const uint8_t *bytes, size_t nbytes, co
             if ((rc = grow((void **)&c->d_hash, &c->d_hash_cap, full, sizeof(uint64_t)))) return rc;
             hashes = c->d_hash;
         }
-        RouteParams p = c->ds.params();
-        DeviceState::add_batch(p, c->d_in, nbytes, c->d_out, cap, hashes, c->d_count, c->d_probed);
-        if ((rc = launch_variant(c->ds, p, c->stream))) return rc;
-        if ((rc = sr_pack_packets(c, c->d_out, c->d_count, cap, f_in, c->ds.dead ? c->d_probed : nullptr,
-                                  c->d_sorted, c->d_packets, pcap, c->d_mcounts, f_out)))
-            return rc;
+        const sr_batch rb{c->d_in, nbytes, c->d_out, cap, hashes, c->d_count, c->d_probed};
+        const sr_pack_batch pb{c->d_out, c->d_count, cap, f_in, c->d_probed, c->d_sorted, c->d_packets, pcap,
+                               c->d_mcounts, f_out};
+        if ((rc = route_pack_impl(c, &rb, &pb, 1))) return rc;
     }
     c->fill_cur ^= 1;
     PackOut o;

@@ -56,7 +56,7 @@ def _oracle_route(oracle, cfg, dead, b, stream, n, alive):
     return _ORACLE[key]
 
 
-def _route_pack_many(pkg, streams, n, alive, fills, layout=None, knobs=()):
+def _route_pack_many(pkg, streams, n, alive, fills, layout=None, knobs=(), fused=False):
     """One sr_route_device_many launch over every batch (probed-dead bitmaps asked for, as the router
     and bench.py do), then ONE sr_pack_packets_many over all of them, each from its own fills."""
     import torch
@@ -84,12 +84,19 @@ def _route_pack_many(pkg, streams, n, alive, fills, layout=None, knobs=()):
             r.set_layout(layout)
         for k, v in knobs:
             r.set_knob(k, v)
-        r.route_device_many([(d_in[b].data_ptr(), int(s.data.size), d_rec[b].data_ptr(), cap, None,
-                              d_cnt[b].data_ptr(), d_pd[b].data_ptr()) for b, s in enumerate(streams)])
-        used_layout = r.last_layout()
-        r.pack_packets_many([(d_rec[b].data_ptr(), d_cnt[b].data_ptr(), cap, d_fin[b].data_ptr(), d_pd[b].data_ptr(),
-                              d_srt[b].data_ptr(), d_pk[b].data_ptr(), mp, d_counts[b].data_ptr(),
-                              d_fout[b].data_ptr()) for b in range(nb)])
+        if fused:   # sr_route_pack_many: the route kernel's tile histograms feed the packing's sort
+            r.route_pack_many([(d_in[b].data_ptr(), int(s.data.size), d_rec[b].data_ptr(), cap, None,
+                                d_cnt[b].data_ptr(), d_pd[b].data_ptr(), d_fin[b].data_ptr(), d_srt[b].data_ptr(),
+                                d_pk[b].data_ptr(), mp, d_counts[b].data_ptr(), d_fout[b].data_ptr())
+                               for b, s in enumerate(streams)])
+            used_layout = r.last_layout()
+        else:
+            r.route_device_many([(d_in[b].data_ptr(), int(s.data.size), d_rec[b].data_ptr(), cap, None,
+                                  d_cnt[b].data_ptr(), d_pd[b].data_ptr()) for b, s in enumerate(streams)])
+            used_layout = r.last_layout()
+            r.pack_packets_many([(d_rec[b].data_ptr(), d_cnt[b].data_ptr(), cap, d_fin[b].data_ptr(), d_pd[b].data_ptr(),
+                                  d_srt[b].data_ptr(), d_pk[b].data_ptr(), mp, d_counts[b].data_ptr(),
+                                  d_fout[b].data_ptr()) for b in range(nb)])
         stream.synchronize()
     out = []
     counts = d_counts.cpu().numpy()
@@ -109,7 +116,13 @@ def _route_pack_many(pkg, streams, n, alive, fills, layout=None, knobs=()):
 
 
 CASES = [
-    # (config, a quarter of the shards dead, batches in the launch, pending bytes in)
+    # (config, a quarter of the shards dead, batches in the launch, pending bytes in[, fused])
+    ("c2", False, 32, "zero", True),   # bench.py's route_pack leg: sr_route_pack_many (tile histograms)
+    ("c2", False, 9, "random", True),
+    ("c3", False, 32, "random", True),
+    ("c4", False, 32, "random", True),
+    ("c5", False, 32, "random", True),   # 64 shards: the counting pass (no histograms)
+    ("c2", True, 32, "random", True),    # dead shards: the counting pass
     ("c2", False, 8, "random"),
     ("c2", False, 9, "random"),
     ("c2", False, 32, "random"),
@@ -124,14 +137,16 @@ CASES = [
 ]
 
 
-@pytest.mark.parametrize("cfg,dead,nb,fill", CASES)
-def test_route_pack_many_full_size(pkg, oracle, cfg, dead, nb, fill):
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "-".join(map(str, c)))
+def test_route_pack_many_full_size(pkg, oracle, case):
+    cfg, dead, nb, fill = case[:4]
+    fused = len(case) > 4 and case[4]
     _, _, _, n, _, _ = _cfg(cfg)
     alive = _alive(cfg, dead)
     streams = _streams(pkg, cfg, nb)
     rng = np.random.default_rng(1000 * nb + n + (7 if dead else 0))
     fills = rng.integers(0, 1451, (nb, n)) if fill == "random" else np.zeros((nb, n), dtype=np.int64)
-    got, _ = _route_pack_many(pkg, streams, n, alive, fills)
+    got, _ = _route_pack_many(pkg, streams, n, alive, fills, fused=fused)
     for b, s in enumerate(streams):
         recs, cnt, probed = _oracle_route(oracle, cfg, dead, b, s, n, alive)
         g = got[b]
@@ -187,3 +202,63 @@ def test_persist_kernel_launch_shapes(pkg, oracle, cfg, nb):
         srt_o, pk_o, fo_o, _ = oracle.pack_packets(recs, n, fills[b], probed)
         assert np.array_equal(got[b]["packets"].view(np.uint8), pk_o.view(np.uint8)), b
         assert got[b]["fill_out"].tolist() == fo_o.tolist(), b
+
+
+def test_route_pack_many_shapes(pkg, oracle):
+    """sr_route_pack_many on shapes its tile-histogram sort must get right: tiles of 2,700 six-byte
+    lines (several 1024-record rounds per group of tiles), empty and one-line batches, 16 shards (the
+    largest with histograms) and 17 (the counting pass), both layouts of the route kernel."""
+    rng = np.random.default_rng(404)
+    shapes = [([6, 7], 3, 1 << 20), ([64, 256, 1024], 16, 1 << 20), ([40, 70, 100, 130], 17, 1 << 20),
+              ([1449, 6], 2, 1 << 19)]
+    for lens, n, size in shapes:
+        streams = [pkg.gen_stream(size - 7919 * b, lens, seed=4040 + b, p_invalid=0.05) for b in range(9)]
+        streams[3] = pkg.Stream(np.zeros(0, np.uint8), np.zeros(0, np.uint32), 0)
+        streams[5] = pkg.gen_stream(40, [13], seed=5)
+        fills = rng.integers(0, 1451, (len(streams), n))
+        for layout in (1, 2):
+            got, _ = _route_pack_many(pkg, streams, n, [1] * n, fills, layout=layout, fused=True)
+            for b, s in enumerate(streams):
+                recs, _, cnt = oracle.route(s.data, n, None) if s.data.size else (np.zeros(0, pkg.RECORD_DTYPE), None, 0)
+                srt_o, pk_o, fo_o, nv_o = oracle.pack_packets(recs, n, fills[b], [])
+                g = got[b]
+                assert g["n_lines"] == cnt, (lens, n, b)
+                assert g["counts"] == (len(pk_o), nv_o, cnt), (lens, n, b, layout)
+                assert np.array_equal(g["sorted"], srt_o), (lens, n, b, layout)
+                assert np.array_equal(g["packets"].view(np.uint8), pk_o.view(np.uint8)), (lens, n, b, layout)
+                assert g["fill_out"].tolist() == fo_o.tolist(), (lens, n, b, layout)
+
+
+def test_route_pack_many_counting_pass_knob(pkg, oracle):
+    """SR_KNOB_HIST 0: sr_route_pack_many with the packing's own counting pass gives the same outputs."""
+    streams = _streams(pkg, "c2", 9)
+    fills = np.random.default_rng(9).integers(0, 1451, (9, 4))
+    a, _ = _route_pack_many(pkg, streams, 4, [1] * 4, fills, fused=True)
+    b, _ = _route_pack_many(pkg, streams, 4, [1] * 4, fills, fused=True, knobs=[(pkg.SR_KNOB_HIST, 0)])
+    for x, y in zip(a, b):
+        assert x["counts"] == y["counts"]
+        assert np.array_equal(x["sorted"], y["sorted"]) and np.array_equal(x["packets"], y["packets"])
+        assert x["fill_out"].tolist() == y["fill_out"].tolist()
+
+
+def test_route_pack_many_rejects_mismatched_batches(pkg):
+    """sr_route_pack_many packs what it routes: a pack batch reading other records is refused."""
+    import torch
+
+    with pkg.Router(4, 1 << 16) as r:
+        a = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+        rec = torch.zeros(1 << 13, dtype=torch.int64, device="cuda")
+        other = torch.zeros(1 << 13, dtype=torch.int64, device="cuda")
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        out = torch.zeros(1 << 14, dtype=torch.int64, device="cuda")
+        fill = torch.zeros(8, dtype=torch.int16, device="cuda")
+        ok = (a.data_ptr(), 100, rec.data_ptr(), 1 << 13, None, cnt.data_ptr(), None, fill.data_ptr(),
+              out.data_ptr(), out.data_ptr() + 8 * 8192, 100, cnt.data_ptr() + 8, fill.data_ptr() + 8)
+        bad = list(ok)
+        bad[2] = other.data_ptr()
+        import ctypes
+        n = 1
+        ra, pa = (pkg.SrBatch * n)(), (pkg.SrPackBatch * n)()
+        ra[0] = pkg.SrBatch(ok[0], ok[1], ok[2], ok[3], None, ok[5], None)
+        pa[0] = pkg.SrPackBatch(bad[2], ok[5], ok[3], ok[7], None, ok[8], ok[9], ok[10], ok[11], ok[12])
+        assert pkg.lib().sr_route_pack_many(r.handle, ra, pa, 1) == -22
