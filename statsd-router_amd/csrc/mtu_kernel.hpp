@@ -286,11 +286,14 @@ __global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuLaunch L) {
     const size_t total = (size_t)nk * ntiles;
     if (tid == 0) carry_s = 0;
     __syncthreads();
-    for (size_t b0 = 0; b0 < total; b0 += 1024 * 4) {
-        uint32_t v[4], s = 0;
+    // 16 entries per thread and round: the route kernel's tile histograms (group mode) are 1024 tiles
+    // per 16 MiB batch, so a batch of 16 shards scans 17 k entries
+    constexpr int kScanPer = 16;
+    for (size_t b0 = 0; b0 < total; b0 += 1024 * kScanPer) {
+        uint32_t v[kScanPer], s = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const size_t i = b0 + (size_t)tid * 4 + k;
+        for (int k = 0; k < kScanPer; ++k) {
+            const size_t i = b0 + (size_t)tid * kScanPer + k;
             v[k] = i < total ? p.tile_counts[i] : 0u;
             s += v[k];
         }
@@ -301,8 +304,8 @@ __global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuLaunch L) {
         for (int w = 0; w < wave; ++w) before += wsum[w];
         uint32_t run = before + incl - s;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const size_t i = b0 + (size_t)tid * 4 + k;
+        for (int k = 0; k < kScanPer; ++k) {
+            const size_t i = b0 + (size_t)tid * kScanPer + k;
             if (i < total) p.tile_counts[i] = run;
             run += v[k];
         }
@@ -433,14 +436,18 @@ __global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_scatter_groups_kernel(
     const uint32_t kbits = nk > 1 ? 32u - (uint32_t)__clz(nk - 1u) : 0u;
     for (uint32_t rb = r0; rb < r1; rb += kMtuTile) {
         const uint32_t re = min(rb + (uint32_t)kMtuTile, r1);
+        const uint32_t rows = (re - rb + 63u) >> 6;   // wave-uniform: a group of long lines is short
         sr_record rr[kMtuPerLane];
-        mtu_load_tile(p, rb, re, lane, rr);
+#pragma unroll
+        for (int k = 0; k < kMtuPerLane; ++k)
+            if ((uint32_t)k < rows) rr[k] = p.recs[min(rb + (uint32_t)(64 * k + lane), re - 1)];
         uint32_t keys[kMtuPerLane];
 #pragma unroll
-        for (int ck = 0; ck < kMtuPerLane; ++ck) keys[ck] = mtu_key(rr[ck], p.nds);
+        for (int ck = 0; ck < kMtuPerLane; ++ck) keys[ck] = (uint32_t)ck < rows ? mtu_key(rr[ck], p.nds) : 0u;
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the round's records are in registers
 #pragma unroll
         for (int ck = 0; ck < kMtuPerLane; ++ck) {
+            if ((uint32_t)ck >= rows) continue;   // wave-uniform
             const uint32_t i = rb + (uint32_t)(64 * ck + lane);
             const bool valid = i < re;
             const uint32_t key = keys[ck];

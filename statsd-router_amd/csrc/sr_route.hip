@@ -475,7 +475,7 @@ static int pack_many_impl(sr_ctx *c, const sr_pack_batch *batches, size_t count,
                                                                             : (uint32_t)kMtuChunk;
     if (c->mtu_chunk) ch = c->mtu_chunk;   // SR_KNOB_MTU_CHUNK (A/B runs)
     uint32_t tiles = 0, chunks = 0, groups = 0;
-    constexpr uint32_t kGroup = 4;   // route tiles per scatter wave (C2: 1024 records)
+    constexpr uint32_t kGroup = 8;   // route tiles per scatter wave (C2: 2048 records, C4: 128)
     for (size_t j = 0; j < count; ++j) {
         const sr_pack_batch &b = batches[j];
         if (!b.d_n_records || !b.d_counts || (nds && !b.d_fill_out) || b.max_records > 0xFFFFFFF0ull) return -EINVAL;
@@ -600,10 +600,16 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
 
 // Route (one launch) and pack. With every shard alive and at most kHistKeys - 1 shards the route
 // kernel (uniform / segment layouts) also writes each tile's key histogram and the packing skips
-// mtu_count, its own pass over the records.
+// mtu_count, its own pass over the records: C2 packing 0.118-0.120 -> 0.108-0.114 ms, C3 0.075-0.077
+// -> 0.069-0.071 per 32 batches. Batches whose record capacity says fewer than 32 lines per 16 KiB
+// tile (C4's 1024-byte lines: 16) keep the counting pass, which is cheaper there than scanning
+// kHistKeys x 1024 tile counts per batch (C4 packing 0.062-0.066 against 0.071-0.076 ms;
+// profiles/r05/pack_hist_ab_r5e.jsonl).
 static int route_pack_impl(sr_ctx *c, const sr_batch *route, const sr_pack_batch *pack, size_t count) {
     DeviceState &ds = c->ds;
-    const bool want = c->hist && ds.dead == 0 && ds.nds >= 1 && ds.nds < (uint32_t)kHistKeys;
+    bool want = c->hist && ds.dead == 0 && ds.nds >= 1 && ds.nds < (uint32_t)kHistKeys;
+    for (size_t i = 0; want && i < count; ++i)
+        want = route[i].max_records * 512 >= route[i].nbytes;
     if (want && !ds.d_hist) {
         const size_t words = (size_t)(ds.max_tiles ? ds.max_tiles : 1) * kHistKeys;
         if (hipMalloc(&ds.d_hist, words * sizeof(uint32_t)) != hipSuccess) ds.d_hist = nullptr;
