@@ -214,7 +214,7 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     if (!(ABL & KV_ALIVE) && p.dead && p.dead < p.nds && p.nds <= 64 * kAliveLds && tid >= (int)kAliveRow0 &&
         (uint32_t)tid < kAliveRow0 + 2 * ((p.nds + 63) / 64))   // the alive words (probe_shard)
         sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)p.alive)[tid - kAliveRow0];
-    if (!(ABL & KV_ALIVE) && p.mark && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
+    if (!(ABL & KV_ALIVE) && p.mark_tiles && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
         sm.img[(uint32_t)tid * 17 + 16] = 0u;
     if (tid == 0) sm.hs[kSlotBefore] = 0ull;
 
@@ -533,7 +533,7 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
             emit(lf, s_abs, len, len_ok, fmt_ok, h);
         }
     }
-    if (!(ABL & KV_ALIVE) && p.mark && bd.probed_dead) {   // MARK_LDS: the dead shards this tile's probes visited
+    if (!(ABL & KV_ALIVE) && p.mark_tiles && bd.probed_dead) {   // MARK_LDS: the dead shards this tile's probes visited
         wg_barrier();
         if ((uint32_t)tid < p.nwords) {
             const uint32_t lo = sm.img[(kMarkRow0 + 2 * (uint32_t)tid) * 17 + 16];

@@ -441,6 +441,9 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
             }
         }
     }
+    // one pick before deferring: every probe that meets a dead shard is deferred and redone whole by
+    // probe_defer_kernel, which notes the dead shards it visits; the route kernel need not
+    p.mark_tiles = (p.mark && !(p.defer && p.picks == 1)) ? 1u : 0u;
     if (ds.wide() && hipMemsetAsync(&ds.d_ctl->pending, 0, sizeof(uint32_t), stream) != hipSuccess) return -EIO;
 #ifdef SR_PERSIST_KERNEL
     if constexpr ((ABL & KV_PERSIST) != 0) {

@@ -183,7 +183,10 @@ struct RouteParams {
     uint32_t nwords;         // alive / probed-dead bitmap words
     uint32_t defer;          // probes past their first `picks` picks are deferred (probe_defer_kernel)
     uint32_t picks;          // with defer: picks the route kernel makes itself (1 or 2)
-    uint32_t mark;           // tiles note the dead shards they probe (LDS, then one atomic per word)
+    uint32_t mark;           // the probes note the dead shards they visit (sr-main.c:106), for the bitmaps
+    uint32_t mark_tiles;     // ... the route kernel's too (LDS words, then its tile slot): not when every
+                             // probe that meets a dead shard is deferred (one pick), which probe_defer_kernel
+                             // then redoes whole, noting its dead picks itself
     Magic magic_n;           // for h % nds (fast path)
     const uint64_t *alive;   // bitmap
     const Magic *magic;      // [0..nds], index i -> divisor i
@@ -719,7 +722,7 @@ __device__ __forceinline__ uint32_t chunk_probe(uint64_t h, const RouteParams &p
                               : (n <= 64 * kAliveLds ? ((alive_pad_dword(img, k) >> (k & 31)) & 1u) != 0
                                                      : alive_bit(p.alive, k));
         if (al) return k;                                                                 // :101-104
-        if (p.mark) note_dead_lds(img, k);                                                // :106
+        if (p.mark_tiles) note_dead_lds(img, k);                                          // :106
         if (j != i - 1) o0 = (j << 16) | (i - 1);                                         // :108-111
         h = (h * 7 + 5) / 3;                                                              // :113
     }
@@ -1556,7 +1559,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 else if (ABL & KV_ALIVE) route = p.nds ? mod_magic(h, p.magic_n, p.nds) : SR_ROUTE_ALL_DEAD;   // :145
                 else if (ABL & KV_PICKS) route = chunk_probe(h, p, sm.img);                          // :145
                 else route = probe_shard(h, p, nullptr, sm.img, nullptr, p.defer != 0,
-                                         p.mark ? sm.img : nullptr);                                // :145
+                                         p.mark_tiles ? sm.img : nullptr);                          // :145
                 // a probe past its first two picks goes to probe_defer_kernel: the record is marked
                 // pending and the hash kept by record index (no counter: same-address atomics from
                 // every wave serialise at the memory side)
@@ -1854,7 +1857,7 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     if (!(ABL & KV_ALIVE) && p.dead && p.dead < p.nds && p.nds <= 64 * kAliveLds && tid >= (int)kAliveRow0 &&
         (uint32_t)tid < kAliveRow0 + 2 * ((p.nds + 63) / 64))   // the alive words (probe_shard)
         sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)p.alive)[tid - kAliveRow0];
-    if (!(ABL & KV_ALIVE) && p.mark && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
+    if (!(ABL & KV_ALIVE) && p.mark_tiles && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
         sm.img[(uint32_t)tid * 17 + 16] = 0u;
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
     if ((ABL & KV_ALIVE) && p.hist && tid < kHistKeys) sm.hist[tid] = 0u;
@@ -1862,7 +1865,7 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     uint32_t c_in;
     tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
     tile_lines<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
-    if (!(ABL & KV_ALIVE) && p.mark && p.b[bi].probed_dead) {   // MARK_LDS: the dead shards this tile's probes visited
+    if (!(ABL & KV_ALIVE) && p.mark_tiles && p.b[bi].probed_dead) {   // MARK_LDS: the dead shards this tile's probes visited
         wg_barrier();
         if ((uint32_t)tid < p.nwords) {   // the tile's slot, ORed by probe_defer_kernel (no atomics)
             const uint32_t lo = sm.img[(kMarkRow0 + 2 * (uint32_t)tid) * 17 + 16];
@@ -1928,7 +1931,7 @@ __global__ __launch_bounds__(256) void probe_defer_kernel(RouteParams p) {
     const bool has_pv = probe_pad_value(p, tid, pv);
     const uint32_t nor = min(gridDim.x, kDeferOrBlocks);
     uint64_t v0 = 0;
-    if (mark && blockIdx.x < nor)
+    if (mark && p.mark_tiles && blockIdx.x < nor)
         for (uint32_t t = blockIdx.x * 256u + tid; t < bd.ntiles; t += nor * 256u)
             v0 |= p.tile_pd[(size_t)(bd.sbase + t) * p.nwords];
     if (blockIdx.x >= nor && blockIdx.x * 4u * kDeferChunk >= n) return;   // uniform over the block
@@ -1942,7 +1945,7 @@ __global__ __launch_bounds__(256) void probe_defer_kernel(RouteParams p) {
     if (has_pv) pads[tid * 17 + 16] = pv;
     if (tid < kReplayCheckWords) wg[tid] = 0ull;
     __syncthreads();
-    if (mark && blockIdx.x < nor) {   // MARK_LDS: the OR of the batch's tile slots, into this block's copy
+    if (mark && p.mark_tiles && blockIdx.x < nor) {   // MARK_LDS: the OR of the batch's tile slots, into this block's copy
         if (v0) atomicOr(&wg[0], (unsigned long long)v0);
         for (uint32_t q = 1; q < p.nwords; ++q) {
             uint64_t v = 0;
