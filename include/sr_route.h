@@ -188,6 +188,23 @@ int sr_pack_many_by_owner(sr_ctx *ctx, const sr_batch *batches, size_t count, ui
                           uint8_t *d_out_bytes, size_t out_cap, sr_record *d_out_recs,
                           uint64_t *d_owner_counts);
 
+/* sr_pack_many_by_owner in two calls, so that the rank's own chunk can be written straight into its
+ * place in the exchange's receive buffers (no local copy in sr_exchange_data):
+ * sr_pack_owner_sizes: the split sizes alone into d_owner_counts (u64 [n_owners][2], as
+ *   sr_pack_many_by_owner's), e.g. for sr_exchange_sizes; the context remembers d_owner_counts.
+ * sr_pack_owner_scatter: the lines and records of the same batches (the next pack call on the context),
+ *   owner `own`'s chunk to d_own_bytes / d_own_recs (its d_owner_counts bytes / lines, offsets relative to
+ *   the chunk as always), every other owner's to d_out_bytes / d_out_recs at the usual places (out_cap as
+ *   sr_pack_many_by_owner). With own = the comm's rank and d_own_* = d_recv_bytes + recv_byte0 /
+ *   d_recv_recs + recv_line0 of peers[rank] (sr_exchange_plan), the following sr_exchange_data on this
+ *   context skips the own chunk's copies. d_own_bytes must be 4-byte aligned. Both asynchronous on the
+ *   context's stream. Returns 0, -EINVAL (scatter without sizes, own out of range), -ENOMEM, -EIO. */
+int sr_pack_owner_sizes(sr_ctx *ctx, const sr_batch *batches, size_t count, uint32_t n_owners,
+                        uint64_t *d_owner_counts);
+int sr_pack_owner_scatter(sr_ctx *ctx, const sr_batch *batches, size_t count, uint32_t n_owners, int own,
+                          uint8_t *d_own_bytes, sr_record *d_own_recs, uint8_t *d_out_bytes, size_t out_cap,
+                          sr_record *d_out_recs);
+
 /* ---- multi-GPU exchange of owner packs (RCCL over xGMI) -------------------------------------- */
 /* One process per GPU; shard s is owned by GPU s % world. After sr_pack_by_owner /
  * sr_pack_many_by_owner (n_owners = world), two collective calls per route launch move every

@@ -50,6 +50,7 @@ ABI_FUNCTIONS = (
     "sr_last_layout",
     "sr_route_batch", "sr_last_probed_dead", "sr_route_device", "sr_route_device_many", "sr_pack_by_owner",
     "sr_pack_many_by_owner", "sr_pack_packets", "sr_pack_packets_many", "sr_route_pack_batch", "sr_alloc_host", "sr_free_host", "sr_sync", "sr_close", "sr_version",
+    "sr_pack_owner_sizes", "sr_pack_owner_scatter",
     "sr_comm_id", "sr_comm_open", "sr_comm_close", "sr_exchange_sizes", "sr_exchange_data",
     "sr_exchange_plan", "sr_exchange_run", "sr_exchange_rebase", "sr_route_pack_submit", "sr_route_pack_result",
     "sr_set_trace", "sr_route_pack_trace", "sr_set_knob", "sr_route_pack_many",
@@ -178,6 +179,9 @@ def _load_route_lib() -> ctypes.CDLL:
                                             vp, ctypes.c_size_t, vp, vp]),
         "sr_pack_many_by_owner": (ctypes.c_int, [vp, ctypes.POINTER(SrBatch), ctypes.c_size_t, ctypes.c_uint32, vp,
                                                  ctypes.c_size_t, vp, vp]),
+        "sr_pack_owner_sizes": (ctypes.c_int, [vp, ctypes.POINTER(SrBatch), ctypes.c_size_t, ctypes.c_uint32, vp]),
+        "sr_pack_owner_scatter": (ctypes.c_int, [vp, ctypes.POINTER(SrBatch), ctypes.c_size_t, ctypes.c_uint32,
+                                                 ctypes.c_int, vp, vp, vp, ctypes.c_size_t, vp]),
         "sr_pack_packets": (ctypes.c_int, [vp, vp, vp, ctypes.c_size_t, vp, vp, vp, vp, ctypes.c_size_t, vp, vp]),
         "sr_pack_packets_many": (ctypes.c_int, [vp, ctypes.POINTER(SrPackBatch), ctypes.c_size_t]),
         "sr_route_pack_batch": (ctypes.c_int, [vp, vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t, c_size_p, c_size_p,
@@ -481,15 +485,34 @@ class Router:
                                          vp(d_probed_dead or 0), vp(d_sorted), vp(d_packets), max_pk, vp(d_counts),
                                          vp(d_fill_out)), "sr_pack_packets")
 
-    def pack_many_by_owner(self, batches, n_owners: int, d_out_bytes: int, out_cap: int, d_out_recs: int,
-                           d_owner_counts: int) -> None:
-        """sr_pack_many_by_owner: batches = [(d_bytes, nbytes, d_recs, max_records, d_n_records), ...]."""
+    @staticmethod
+    def _owner_batches(batches):
         arr = (SrBatch * max(len(batches), 1))()
         for i, (db, nb, dr, mr, dn) in enumerate(batches):
             arr[i] = SrBatch(db, nb, dr, mr, None, dn, None)
+        return arr
+
+    def pack_many_by_owner(self, batches, n_owners: int, d_out_bytes: int, out_cap: int, d_out_recs: int,
+                           d_owner_counts: int) -> None:
+        """sr_pack_many_by_owner: batches = [(d_bytes, nbytes, d_recs, max_records, d_n_records), ...]."""
         vp = ctypes.c_void_p
-        _check(self._lib.sr_pack_many_by_owner(self._h, arr, len(batches), n_owners, vp(d_out_bytes), out_cap,
-                                               vp(d_out_recs), vp(d_owner_counts)), "sr_pack_many_by_owner")
+        _check(self._lib.sr_pack_many_by_owner(self._h, self._owner_batches(batches), len(batches), n_owners,
+                                               vp(d_out_bytes), out_cap, vp(d_out_recs), vp(d_owner_counts)),
+               "sr_pack_many_by_owner")
+
+    def pack_owner_sizes(self, batches, n_owners: int, d_owner_counts: int) -> None:
+        """sr_pack_owner_sizes: the split sizes of sr_pack_many_by_owner alone (batches as there)."""
+        _check(self._lib.sr_pack_owner_sizes(self._h, self._owner_batches(batches), len(batches), n_owners,
+                                             ctypes.c_void_p(d_owner_counts)), "sr_pack_owner_sizes")
+
+    def pack_owner_scatter(self, batches, n_owners: int, own: int, d_own_bytes: int, d_own_recs: int,
+                           d_out_bytes: int, out_cap: int, d_out_recs: int) -> None:
+        """sr_pack_owner_scatter: the rest of the pack after pack_owner_sizes, owner `own`'s chunk written to
+        d_own_bytes / d_own_recs (e.g. its place in the exchange's receive buffers)."""
+        vp = ctypes.c_void_p
+        _check(self._lib.sr_pack_owner_scatter(self._h, self._owner_batches(batches), len(batches), n_owners, own,
+                                               vp(d_own_bytes), vp(d_own_recs), vp(d_out_bytes), out_cap,
+                                               vp(d_out_recs)), "sr_pack_owner_scatter")
 
     def pack_packets_many(self, batches) -> None:
         """sr_pack_packets_many: batches = [(d_recs, d_n_records, max_records, d_fill_in, d_probed_dead,

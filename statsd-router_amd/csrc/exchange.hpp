@@ -128,7 +128,7 @@ inline int rebase_args(const sr_exchange_peer *peers, int world, RebaseArgs &a) 
 // is q's receive size from me), the own chunk, then the rebase.
 inline int exchange_run(const sr_transport &t, int world, int rank, const uint64_t *sent, const uint64_t *received,
                         const uint8_t *packed, const sr_record *packed_recs, uint8_t *recv_bytes,
-                        sr_record *recv_recs) {
+                        sr_record *recv_recs, bool own_in_place = false) {
     if (!t.group_start || !t.group_end || !t.send || !t.recv || !t.copy || !t.rebase) return -EINVAL;
     sr_exchange_peer peers[kMaxOwners];
     uint64_t tot[4];
@@ -155,11 +155,12 @@ inline int exchange_run(const sr_transport &t, int world, int rank, const uint64
     rc = t.group_end(t.user);   // always closed, also after a failed post
     if (bad) return bad;
     if (rc) return rc;
-    const sr_exchange_peer &own = peers[rank];
-    if (own.send_bytes && (rc = t.copy(t.user, recv_bytes + own.recv_byte0, packed + own.send_byte0, own.send_bytes)))
+    const sr_exchange_peer &own = peers[rank];   // (own_in_place: the pack wrote it there)
+    if (!own_in_place && own.send_bytes &&
+        (rc = t.copy(t.user, recv_bytes + own.recv_byte0, packed + own.send_byte0, own.send_bytes)))
         return rc;
-    if (own.send_lines && (rc = t.copy(t.user, recv_recs + own.recv_line0, packed_recs + own.send_line0,
-                                       own.send_lines * sizeof(sr_record))))
+    if (!own_in_place && own.send_lines &&
+        (rc = t.copy(t.user, recv_recs + own.recv_line0, packed_recs + own.send_line0, own.send_lines * sizeof(sr_record))))
         return rc;
     return tot[2] ? t.rebase(t.user, recv_recs, peers, world, tot[2]) : 0;
 }

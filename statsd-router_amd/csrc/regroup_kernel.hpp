@@ -52,6 +52,12 @@ struct PackParams {
     uint8_t *out_bytes;
     uint64_t out_cap;
     sr_record *out_recs;
+    // sr_pack_owner_scatter: owner `own`'s chunk goes to own_bytes / own_recs (its place in the
+    // exchange's receive buffers; capacity: its own byte count) instead of out_*; -1: none
+    int32_t own;
+    uint32_t pad2;
+    uint8_t *own_bytes;
+    sr_record *own_recs;
     PackBatch b[kPackMaxBatches];
 };
 
@@ -203,16 +209,20 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
                 pb += s_wb[w][ow];
             }
             const uint2 tb = p.tile_base[(size_t)blockIdx.x * G + ow];
-            const uint64_t line = p.owner_start[2 * ow] + tb.x + pl + my_l;
             const uint32_t rel = tb.y + pb + my_b;   // byte position within the owner's chunk
-            dst = (uint32_t)(p.owner_start[2 * ow + 1] + rel);
             sr_record o = r;
             o.offset = rel;
-            p.out_recs[line] = o;
+            if (ow == p.own) {   // straight into its place in the receive buffers
+                dst = rel;
+                p.own_recs[tb.x + pl + my_l] = o;
+            } else {
+                dst = (uint32_t)(p.owner_start[2 * ow + 1] + rel);
+                p.out_recs[p.owner_start[2 * ow] + tb.x + pl + my_l] = o;
+            }
         }
         s_src[tid] = r.offset;
         s_dst[tid] = dst;
-        s_len[tid] = ow >= 0 ? r.length : 0u;
+        s_len[tid] = ow >= 0 ? r.length | (ow == p.own ? 0x80000000u : 0u) : 0u;
         __syncthreads();
         if (tid < (int)G) {
             uint32_t al = 0, ab = 0;
@@ -230,9 +240,14 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
         // the loads of kCopyBatch passes are issued before their stores
         constexpr int kCopyBatch = 4;
         const int sub = tid & 15;
+        const uint64_t own_cap = p.own >= 0 ? p.owner_counts[2 * p.own + 1] : 0ull;
         for (int k = tid >> 4; k < kPackBlock; k += kPackBlock / 16) {
-            const uint32_t L = s_len[k];
-            if (L == 0) continue;
+            const uint32_t Lf = s_len[k];
+            if (Lf == 0) continue;
+            const bool mine = (Lf >> 31) != 0;
+            const uint32_t L = Lf & 0x7FFFFFFFu;
+            uint8_t *const out = mine ? p.own_bytes : p.out_bytes;
+            const uint64_t cap = mine ? own_cap : p.out_cap;
             const uint32_t src = s_src[k], d = s_dst[k];
             const uint32_t sh = src & 3u, sa = src & ~3u;
             const uint32_t L4 = pack_len4(L);
@@ -260,13 +275,13 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
                         if (qj >= L) w[j] = 0;
                         else if (qj + 4u > L) w[j] &= (1u << (8u * (L - qj))) - 1u;
                     }
-                    uint8_t *o = p.out_bytes + d + q;
-                    if (q + 16u <= L4 && (uint64_t)d + q + 16u <= p.out_cap) {
+                    uint8_t *o = out + d + q;
+                    if (q + 16u <= L4 && (uint64_t)d + q + 16u <= cap) {
                         *(uint4 *)o = make_uint4(w[0], w[1], w[2], w[3]);
                     } else {
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
-                            if (q + 4u * j < L4 && (uint64_t)d + q + 4u * j + 4u <= p.out_cap) ((uint32_t *)o)[j] = w[j];
+                            if (q + 4u * j < L4 && (uint64_t)d + q + 4u * j + 4u <= cap) ((uint32_t *)o)[j] = w[j];
                     }
                 }
             }

@@ -45,6 +45,13 @@ struct sr_ctx {
     uint32_t *d_mtu_tiles, *d_mtu_keys, *d_mtu_chunks;
     uint64_t *d_mtu_table;
     uint32_t *d_mtu_gp;    // per chunk: bytes per packet start (kMtuChunk u16), then the first prefix sums
+    // sr_pack_owner_sizes / sr_pack_owner_scatter: the split sizes of the pack in progress, and where its
+    // scatter wrote owner `own`'s chunk (sr_exchange_data then skips that chunk's copy)
+    uint64_t *own_counts;
+    uint64_t own_shape;   // n_owners and the batches' tile count of that pack (the scatter must match)
+    int own_set, own;
+    uint8_t *own_bytes;
+    sr_record *own_recs;
     // buffers of sr_route_pack_batch
     sr_record *d_sorted;
     size_t d_sorted_cap;
@@ -332,8 +339,12 @@ int sr_route_device_many(sr_ctx *c, const sr_batch *batches, size_t count) {
     return 0;
 }
 
+// The owner pack: kPackSizes = count + scan (the split sizes into d_owner_counts), kPackScatter =
+// the lines and records (owner `own` into own_bytes / own_recs when own >= 0)
+enum : int { kPackSizes = 1, kPackScatter = 2 };
 static int pack_launch(sr_ctx *c, const PackBatch *in, uint32_t nb, uint32_t n_owners, uint8_t *d_out_bytes,
-                       size_t out_cap, sr_record *d_out_recs, uint64_t *d_owner_counts) {
+                       size_t out_cap, sr_record *d_out_recs, uint64_t *d_owner_counts, int phases = kPackSizes | kPackScatter,
+                       int own = -1, uint8_t *own_bytes = nullptr, sr_record *own_recs = nullptr) {
     PackParams p;
     memset(&p, 0, sizeof(p));
     uint32_t ntiles = 0;
@@ -362,13 +373,18 @@ static int pack_launch(sr_ctx *c, const PackBatch *in, uint32_t nb, uint32_t n_o
     p.out_bytes = d_out_bytes;
     p.out_cap = out_cap;
     p.out_recs = d_out_recs;
-    if (ntiles) {
+    p.own = own;
+    p.own_bytes = own_bytes;
+    p.own_recs = own_recs;
+    if ((phases & kPackSizes) && ntiles) {
         hipLaunchKernelGGL(pack_count_kernel, dim3(ntiles), dim3(kPackBlock), 0, c->stream, p);
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
-    hipLaunchKernelGGL(pack_scan_kernel, dim3(1), dim3(1024), 0, c->stream, p);
-    if (hipGetLastError() != hipSuccess) return -EIO;
-    if (ntiles) {
+    if (phases & kPackSizes) {
+        hipLaunchKernelGGL(pack_scan_kernel, dim3(1), dim3(1024), 0, c->stream, p);
+        if (hipGetLastError() != hipSuccess) return -EIO;
+    }
+    if ((phases & kPackScatter) && ntiles) {
         hipLaunchKernelGGL(pack_scatter_kernel, dim3(ntiles), dim3(kPackBlock), 0, c->stream, p);
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
@@ -387,27 +403,83 @@ int sr_pack_by_owner(sr_ctx *c, const uint8_t *d_bytes, size_t nbytes, const sr_
     if (max_records && (!d_recs || !d_out_recs || !d_bytes || !d_out_bytes)) return -EINVAL;
     (void)hipSetDevice(c->device);
     PackBatch b{d_bytes, d_recs, d_n_records, (uint32_t)nbytes, (uint32_t)max_records, 0, 0};
+    c->own_set = 0;
+    c->own_counts = nullptr;
     return pack_launch(c, &b, 1, n_owners, d_out_bytes, out_cap, d_out_recs, d_owner_counts);
 }
 
-int sr_pack_many_by_owner(sr_ctx *c, const sr_batch *batches, size_t count, uint32_t n_owners, uint8_t *d_out_bytes,
-                          size_t out_cap, sr_record *d_out_recs, uint64_t *d_owner_counts) {
-    if (!c || !d_owner_counts || n_owners == 0 || n_owners > SR_MAX_OWNERS) return -EINVAL;
+static uint64_t pack_shape(const PackBatch *in, size_t count, uint32_t n_owners) {
+    uint64_t tiles = 0;
+    for (size_t j = 0; j < count; ++j) tiles += (in[j].max_records + kPackTile - 1) / kPackTile;
+    return tiles << 8 | n_owners;
+}
+
+static int pack_many_args(const sr_batch *batches, size_t count, uint32_t n_owners, PackBatch *in,
+                          uint64_t *total_bytes) {
+    if (n_owners == 0 || n_owners > SR_MAX_OWNERS) return -EINVAL;
     if (count == 0 || count > SR_MAX_BATCHES_PER_LAUNCH || !batches) return -EINVAL;
-    uint64_t total_bytes = 0;
-    PackBatch in[kPackMaxBatches];
+    *total_bytes = 0;
     for (size_t j = 0; j < count; ++j) {
         const sr_batch &b = batches[j];
         if (!b.d_n_records || b.max_records > 0xFFFFFFFFull || b.nbytes > 0xFFFFFFF0ull) return -EINVAL;
         if (b.max_records && (!b.d_out || !b.d_bytes)) return -EINVAL;
-        total_bytes += b.nbytes;
+        *total_bytes += b.nbytes;
         in[j] = PackBatch{b.d_bytes, b.d_out, b.d_n_records, (uint32_t)b.nbytes, (uint32_t)b.max_records, 0, 0};
     }
-    if (SR_PACK_CAPACITY(total_bytes) > 0xFFFFFFFFull || out_cap < SR_PACK_CAPACITY(total_bytes)) return -EINVAL;
+    return SR_PACK_CAPACITY(*total_bytes) > 0xFFFFFFFFull ? -EINVAL : 0;
+}
+
+int sr_pack_many_by_owner(sr_ctx *c, const sr_batch *batches, size_t count, uint32_t n_owners, uint8_t *d_out_bytes,
+                          size_t out_cap, sr_record *d_out_recs, uint64_t *d_owner_counts) {
+    if (!c || !d_owner_counts) return -EINVAL;
+    uint64_t total_bytes = 0;
+    PackBatch in[kPackMaxBatches];
+    int rc = pack_many_args(batches, count, n_owners, in, &total_bytes);
+    if (rc) return rc;
+    if (out_cap < SR_PACK_CAPACITY(total_bytes)) return -EINVAL;
     if (out_cap > 0xFFFFFFFFull) out_cap = 0xFFFFFFFFull;
     if (!d_out_bytes || !d_out_recs) return -EINVAL;
     (void)hipSetDevice(c->device);
+    c->own_set = 0;
+    c->own_counts = nullptr;
     return pack_launch(c, in, (uint32_t)count, n_owners, d_out_bytes, out_cap, d_out_recs, d_owner_counts);
+}
+
+int sr_pack_owner_sizes(sr_ctx *c, const sr_batch *batches, size_t count, uint32_t n_owners, uint64_t *d_owner_counts) {
+    if (!c || !d_owner_counts) return -EINVAL;
+    uint64_t total_bytes = 0;
+    PackBatch in[kPackMaxBatches];
+    int rc = pack_many_args(batches, count, n_owners, in, &total_bytes);
+    if (rc) return rc;
+    (void)hipSetDevice(c->device);
+    c->own_set = 0;
+    c->own_counts = d_owner_counts;
+    c->own_shape = pack_shape(in, count, n_owners);
+    rc = pack_launch(c, in, (uint32_t)count, n_owners, nullptr, 0, nullptr, d_owner_counts, kPackSizes);
+    if (rc) c->own_counts = nullptr;
+    return rc;
+}
+
+int sr_pack_owner_scatter(sr_ctx *c, const sr_batch *batches, size_t count, uint32_t n_owners, int own,
+                          uint8_t *d_own_bytes, sr_record *d_own_recs, uint8_t *d_out_bytes, size_t out_cap,
+                          sr_record *d_out_recs) {
+    if (!c || !c->own_counts || own < 0 || (uint32_t)own >= n_owners) return -EINVAL;
+    uint64_t total_bytes = 0;
+    PackBatch in[kPackMaxBatches];
+    int rc = pack_many_args(batches, count, n_owners, in, &total_bytes);
+    if (rc) return rc;
+    if (pack_shape(in, count, n_owners) != c->own_shape) return -EINVAL;
+    if (out_cap < SR_PACK_CAPACITY(total_bytes)) return -EINVAL;
+    if (out_cap > 0xFFFFFFFFull) out_cap = 0xFFFFFFFFull;
+    if (!d_out_bytes || !d_out_recs || !d_own_bytes || !d_own_recs || ((uintptr_t)d_own_bytes & 3u)) return -EINVAL;
+    (void)hipSetDevice(c->device);
+    // sr_exchange_data finds the own chunk in place and does not copy it
+    c->own_set = 1;
+    c->own = own;
+    c->own_bytes = d_own_bytes;
+    c->own_recs = d_own_recs;
+    return pack_launch(c, in, (uint32_t)count, n_owners, d_out_bytes, out_cap, d_out_recs, c->own_counts, kPackScatter,
+                       own, d_own_bytes, d_own_recs);
 }
 
 // Scratch of the packing kernels for one launch (grown, never shrunk; not in stream capture).
@@ -1044,8 +1116,19 @@ int sr_exchange_data(sr_ctx *ctx, sr_comm *comm, const uint8_t *d_packed, const 
     (void)hipSetDevice(ctx->device);
     RcclTransport rt{r, comm, ctx->stream};
     const sr_transport t{&rt, rccl_group_start, rccl_group_end, rccl_send, rccl_recv, rccl_copy, rccl_rebase};
+    // the own chunk already in its place (sr_pack_owner_scatter into these receive buffers): no copy
+    bool in_place = false;
+    if (ctx->own_set && ctx->own == comm->rank) {
+        sr_exchange_peer peers[kMaxOwners];
+        uint64_t tot[4];
+        if (exchange_plan(comm->world, comm->rank, h_sent, h_received, peers, tot) == 0) {
+            const sr_exchange_peer &e = peers[comm->rank];
+            in_place = ctx->own_bytes == d_recv_bytes + e.recv_byte0 && ctx->own_recs == d_recv_recs + e.recv_line0;
+        }
+    }
+    ctx->own_set = 0;
     return exchange_run(t, comm->world, comm->rank, h_sent, h_received, d_packed, d_packed_recs, d_recv_bytes,
-                        d_recv_recs);
+                        d_recv_recs, in_place);
 }
 
 int sr_exchange_plan(int world, int rank, const uint64_t *h_sent, const uint64_t *h_received,

@@ -216,10 +216,14 @@ class LaunchRegrouper:
     all-to-all of the split sizes with one host round trip, then the packed lines and the records
     (RCCL over xGMI with the "nccl" backend; gloo in the CPU tests). Same stream rule as Regrouper."""
 
-    def __init__(self, pkg, router, max_total_bytes: int, max_total_records: int, group=None, comm=None):
+    def __init__(self, pkg, router, max_total_bytes: int, max_total_records: int, group=None, comm=None,
+                 own_in_place: bool = True):
         """comm: a pkg.Comm for the C-ABI exchange (sr_exchange_sizes / sr_exchange_data over RCCL);
-        None: torch.distributed collectives on `group` (gloo in the CPU tests, nccl on GPUs)."""
+        None: torch.distributed collectives on `group` (gloo in the CPU tests, nccl on GPUs).
+        own_in_place (C-ABI exchange): the pack writes the rank's own chunk straight into the receive
+        buffers; False: one sr_pack_many_by_owner and a device copy of the own chunk (A/B runs)."""
         self.pkg, self.router, self.group, self.comm = pkg, router, group, comm
+        self.own_in_place = own_in_place
         self.G = dist.get_world_size(group)
         if not 1 <= self.G <= pkg.SR_MAX_OWNERS:
             raise ValueError(f"regroup over {self.G} ranks: at most {pkg.SR_MAX_OWNERS}")
@@ -247,13 +251,19 @@ class LaunchRegrouper:
                                "required (for the torch.distributed exchange: torch's current stream)")
         if sum(b[3] for b in batches) > self.max_records or self.pkg.pack_capacity(sum(b[1] for b in batches)) > self.cap:
             raise ValueError("launch larger than the regrouper's buffers")
-        self.router.pack_many_by_owner(batches, self.G, self.bytes.data_ptr(), self.cap, self.recs.data_ptr(),
-                                       self.counts.data_ptr())
         if self.comm is None:
+            self.router.pack_many_by_owner(batches, self.G, self.bytes.data_ptr(), self.cap, self.recs.data_ptr(),
+                                           self.counts.data_ptr())
             rb, rr, rc, self.last_sent, self.last_received = _exchange(self.bytes, self.recs, self.counts, self.group)
             return rb, rr, rc
-        # the C ABI: one size exchange (one host round trip), then the grouped sends and the rebase;
-        # receive buffers from the caching allocator's pool of the router's stream
+        # the C ABI: the split sizes, one size exchange (one host round trip), then the scatter with the
+        # rank's own chunk written straight into its place in the receive buffers (no local copy), the
+        # grouped sends and the rebase; receive buffers from the caching allocator's pool of the router's stream
+        if self.own_in_place:
+            self.router.pack_owner_sizes(batches, self.G, self.counts.data_ptr())
+        else:
+            self.router.pack_many_by_owner(batches, self.G, self.bytes.data_ptr(), self.cap, self.recs.data_ptr(),
+                                           self.counts.data_ptr())
         rs = torch.cuda.ExternalStream(h, device=self.bytes.device) if h != cur else torch.cuda.current_stream()
         with torch.cuda.stream(rs):
             rc = torch.empty((self.G, 2), dtype=torch.int64, device=self.bytes.device)
@@ -261,6 +271,12 @@ class LaunchRegrouper:
             n_l, n_b = int(received[:, 0].sum()), int(received[:, 1].sum())
             rb = torch.empty(max(n_b, 1), dtype=torch.uint8, device=self.bytes.device)
             rr = torch.empty(max(n_l, 1), dtype=torch.int64, device=self.bytes.device)
+        if self.own_in_place:
+            peers, _ = self.pkg.exchange_plan(self.G, self.comm.rank, sent, received)
+            me = peers[self.comm.rank]
+            self.router.pack_owner_scatter(batches, self.G, self.comm.rank, rb.data_ptr() + int(me["recv_byte0"]),
+                                       rr.data_ptr() + 8 * int(me["recv_line0"]), self.bytes.data_ptr(), self.cap,
+                                           self.recs.data_ptr())
         self.router.exchange_data(self.comm, self.bytes.data_ptr(), self.recs.data_ptr(), sent, received,
                                   rb.data_ptr(), rr.data_ptr())
         self.last_sent, self.last_received = sent.astype(np.int64).tolist(), received.astype(np.int64).tolist()

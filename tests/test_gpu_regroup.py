@@ -379,3 +379,108 @@ def test_exchange_run_device_three_ranks(pkg, oracle):
         lines = [bytes(pb[int(cnt[:r, 1].sum()) + x["offset"]:][: x["length"]])
                  for pb, pr, cnt in packs for x in pr[int(cnt[:r, 0].sum()):][: int(cnt[r, 0])]]
         assert [bytes(rb[x["offset"]: x["offset"] + x["length"]]) for x in rr] == lines
+
+
+@pytest.mark.parametrize("G,own", [(1, 0), (3, 1), (8, 7), (8, 0)])
+def test_pack_owner_split_matches_oracle(pkg, oracle, G, own, torch_stream):
+    """sr_pack_owner_sizes + sr_pack_owner_scatter = sr_pack_many_by_owner, with owner `own`'s chunk in its
+    own buffers (nothing of it in the packed buffer, nothing written past it); a scatter whose batches do not
+    match the sizes call, or without one, is refused."""
+    import torch
+
+    nb, n_shards = 3, 64
+    streams = [pkg.gen_stream(1 << 18, [64, 256, 1024], seed=1300 + 11 * G + b, p_invalid=0.05) for b in range(nb)]
+    cap = max(s.n_lines for s in streams)
+    d_in = torch.zeros((nb, 1 << 18), dtype=torch.uint8, device="cuda")
+    for b, s in enumerate(streams):
+        d_in[b, : s.data.size].copy_(torch.from_numpy(s.data))
+    d_rec = torch.zeros((nb, cap), dtype=torch.int64, device="cuda")
+    d_n = torch.zeros(nb, dtype=torch.int64, device="cuda")
+    out_cap = pkg.pack_capacity(sum(int(s.data.size) for s in streams))
+    d_pb = torch.full((out_cap,), 0xAB, dtype=torch.uint8, device="cuda")
+    d_pr = torch.full((nb * cap,), -1, dtype=torch.int64, device="cuda")
+    d_cnt = torch.zeros((G, 2), dtype=torch.int64, device="cuda")
+    batches = [(d_in[b].data_ptr(), int(s.data.size), d_rec[b].data_ptr(), cap, d_n[b].data_ptr())
+               for b, s in enumerate(streams)]
+    with pkg.Router(n_shards, 1 << 18) as r:
+        r.set_stream(torch_stream.cuda_stream)
+        r.route_device_many([(db, n, dr, mr, None, dn) for db, n, dr, mr, dn in batches])
+        with pytest.raises(pkg.SrError):   # no sizes call yet
+            r.pack_owner_scatter(batches, G, own, d_pb.data_ptr(), d_pr.data_ptr(), d_pb.data_ptr(), out_cap,
+                                 d_pr.data_ptr())
+        r.pack_owner_sizes(batches, G, d_cnt.data_ptr())
+        torch.cuda.synchronize()
+        cnt = d_cnt.cpu().numpy()
+        ob = torch.full((int(cnt[own, 1]) + 256,), 0xCD, dtype=torch.uint8, device="cuda")
+        orr = torch.full((int(cnt[own, 0]) + 8,), -1, dtype=torch.int64, device="cuda")
+        with pytest.raises(pkg.SrError):   # other batches than the sizes call's
+            r.pack_owner_scatter(batches[:2], G, own, ob.data_ptr(), orr.data_ptr(), d_pb.data_ptr(), out_cap,
+                                 d_pr.data_ptr())
+        with pytest.raises(pkg.SrError):
+            r.pack_owner_scatter(batches, G, G, ob.data_ptr(), orr.data_ptr(), d_pb.data_ptr(), out_cap, d_pr.data_ptr())
+        r.pack_owner_scatter(batches, G, own, ob.data_ptr(), orr.data_ptr(), d_pb.data_ptr(), out_cap, d_pr.data_ptr())
+        torch.cuda.synchronize()
+    recs_list = [oracle.route(s.data, n_shards)[0] for s in streams]
+    eb, er, ec = oracle.pack_many_by_owner([s.data for s in streams], recs_list, G)
+    assert cnt.tolist() == ec.tolist()
+    l0 = np.concatenate([[0], np.cumsum(ec[:, 0])]).astype(np.int64)
+    b0 = np.concatenate([[0], np.cumsum(ec[:, 1])]).astype(np.int64)
+    got_b = d_pb.cpu().numpy()
+    got_r = np.frombuffer(d_pr.cpu().numpy().tobytes(), dtype=pkg.RECORD_DTYPE)
+    for o in range(G):
+        if o == own:
+            assert (got_b[b0[o]: b0[o + 1]] == 0xAB).all()
+            assert (d_pr.cpu().numpy()[l0[o]: l0[o + 1]] == -1).all()
+        else:
+            assert np.array_equal(got_b[b0[o]: b0[o + 1]], eb[b0[o]: b0[o + 1]])
+            assert np.array_equal(got_r[l0[o]: l0[o + 1]], er[l0[o]: l0[o + 1]])
+    mine_b = ob.cpu().numpy()
+    assert np.array_equal(mine_b[: ec[own, 1]], eb[b0[own]: b0[own + 1]]) and (mine_b[ec[own, 1]:] == 0xCD).all()
+    mine_r = orr.cpu().numpy()
+    assert np.array_equal(mine_r[: ec[own, 0]].view(pkg.RECORD_DTYPE), er[l0[own]: l0[own + 1]])
+    assert (mine_r[ec[own, 0]:] == -1).all()
+
+
+def test_c_exchange_own_chunk_in_place(pkg, oracle, torch_stream):
+    """One-rank RCCL exchange after sr_pack_owner_scatter into the receive buffers: sr_exchange_data
+    does not copy the (never written) packed own chunk over it, and the result is the oracle's pack."""
+    import torch
+
+    streams = [pkg.gen_stream(1 << 19, [64, 256, 1024], seed=720 + b, p_invalid=0.05) for b in range(2)]
+    cap = max(s.n_lines for s in streams)
+    d_in = torch.zeros((2, 1 << 19), dtype=torch.uint8, device="cuda")
+    for b, s in enumerate(streams):
+        d_in[b, : s.data.size].copy_(torch.from_numpy(s.data))
+    d_rec = torch.zeros((2, cap), dtype=torch.int64, device="cuda")
+    d_n = torch.zeros(2, dtype=torch.int64, device="cuda")
+    out_cap = pkg.pack_capacity(sum(int(s.data.size) for s in streams))
+    d_pb = torch.full((out_cap,), 0xAB, dtype=torch.uint8, device="cuda")
+    d_pr = torch.zeros(2 * cap, dtype=torch.int64, device="cuda")
+    d_cnt = torch.zeros((1, 2), dtype=torch.int64, device="cuda")
+    d_rc = torch.zeros((1, 2), dtype=torch.int64, device="cuda")
+    comm = pkg.Comm(pkg.Comm.new_id(), 1, 0, 0)
+    try:
+        with pkg.Router(32, 1 << 19) as r:
+            r.set_stream(torch_stream.cuda_stream)
+            batches = [(d_in[b].data_ptr(), int(s.data.size), d_rec[b].data_ptr(), cap, d_n[b].data_ptr())
+                       for b, s in enumerate(streams)]
+            r.route_device_many([(db, nb, dr, mr, None, dn) for db, nb, dr, mr, dn in batches])
+            r.pack_owner_sizes(batches, 1, d_cnt.data_ptr())
+            sent, received = r.exchange_sizes(comm, d_cnt.data_ptr(), d_rc.data_ptr())
+            n_l, n_b = int(received[:, 0].sum()), int(received[:, 1].sum())
+            rb = torch.full((n_b + 64,), 0xCD, dtype=torch.uint8, device="cuda")
+            rr = torch.zeros(n_l, dtype=torch.int64, device="cuda")
+            peers, _ = pkg.exchange_plan(1, 0, sent, received)
+            r.pack_owner_scatter(batches, 1, 0, rb.data_ptr() + int(peers[0]["recv_byte0"]),
+                                 rr.data_ptr() + 8 * int(peers[0]["recv_line0"]), d_pb.data_ptr(), out_cap,
+                                 d_pr.data_ptr())
+            r.exchange_data(comm, d_pb.data_ptr(), d_pr.data_ptr(), sent, received, rb.data_ptr(), rr.data_ptr())
+            r.sync()
+    finally:
+        comm.close()
+    recs_list = [oracle.route(s.data, 32)[0] for s in streams]
+    eb, er, ec = oracle.pack_many_by_owner([s.data for s in streams], recs_list, 1)
+    got_b = rb.cpu().numpy()
+    assert np.array_equal(got_b[:n_b], eb) and (got_b[n_b:] == 0xCD).all()
+    assert np.array_equal(rr.cpu().numpy().view(pkg.RECORD_DTYPE), er)
+    assert (d_pb.cpu().numpy() == 0xAB).all()   # the packed buffer was never needed
