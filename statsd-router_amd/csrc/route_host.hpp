@@ -490,8 +490,9 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
         hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     }
     if (hipGetLastError() != hipSuccess) return -EIO;
-    // the key histograms exist only where route_kernel counted them (every shard alive)
-    ds.last_hist = p.hist && (ABL & KV_ALIVE) && !(ABL & KV_CHUNKS);
+    // the key histograms exist only where route_kernel counted them with every route final: every shard
+    // alive, or the picks-only probe without deferral (one dead shard: two picks always end it)
+    ds.last_hist = p.hist && (ABL & (KV_ALIVE | KV_PICKS)) && !(ABL & KV_CHUNKS) && !p.defer && ds.dead <= 1;
     if (p.defer || p.mark) {   // the probes past their first two picks and the OR of the tiles' probed-dead
                                // slots (probe_defer_kernel), grid y = batch
         // blocks past a batch's record count return at once; the rest loop over chunks of 4 waves

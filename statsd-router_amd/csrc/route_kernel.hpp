@@ -1579,7 +1579,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 }
                 const uint32_t rec = base + (uint32_t)j;
                 if (rec < bd.max_records) {
-                    if constexpr ((ABL & KV_ALIVE) != 0)   // the packing's key histogram (ds_add, no return)
+                    if constexpr ((ABL & (KV_ALIVE | KV_PICKS)) != 0)   // the packing's key histogram (ds_add, no return)
                         if (p.hist) atomicAdd(&sm.hist[route < p.nds ? route : p.nds], 1u);
                     if (deferred) bd.dhash[rec] = h;
                     if (!(ABL & KV_ALIVE) && route == kRoutePending && !deferred) {
@@ -1860,7 +1860,7 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     if (!(ABL & KV_ALIVE) && p.mark_tiles && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
         sm.img[(uint32_t)tid * 17 + 16] = 0u;
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
-    if ((ABL & KV_ALIVE) && p.hist && tid < kHistKeys) sm.hist[tid] = 0u;
+    if ((ABL & (KV_ALIVE | KV_PICKS)) && p.hist && tid < kHistKeys) sm.hist[tid] = 0u;
     uint64_t nlm, clm;
     uint32_t c_in;
     tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
@@ -1873,7 +1873,7 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
             p.tile_pd[(size_t)(p.b[bi].sbase + t) * p.nwords + tid] = ((uint64_t)hi << 32) | lo;
         }
     }
-    if ((ABL & KV_ALIVE) && p.hist) {   // the tile's key histogram for the packing (sr_route_pack_many)
+    if ((ABL & (KV_ALIVE | KV_PICKS)) && p.hist) {   // the tile's key histogram for the packing (sr_route_pack_many)
         wg_barrier();
         const BatchDesc &bd = p.b[bi];
         if ((uint32_t)tid <= p.nds)

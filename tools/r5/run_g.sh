@@ -15,3 +15,10 @@ for r in 1 2; do
     done
   done
 done
+# kernel stats of the route + pack leg (C2, C5) on this build
+export TMPDIR=/tmp
+R=$(pwd)
+for c in c2 c5; do
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/r5g_prof_$c" -o run \
+     -- python "$R/bench.py" --config $c --no-cpu --no-e2e --regroup off --steps 50 --warmup 10 > "$R/$O/r5g_prof_$c.json" 2> "$R/$O/r5g_prof_$c.err") || exit 1
+done
