@@ -410,7 +410,10 @@ int sr_route_pack_trace(sr_ctx *ctx, int slot, const sr_record **records, const 
  *                         1 in the chunk layout, 2 in every layout (developer builds only, measured
  *                         slower: -ENOTSUP otherwise);
  *   SR_KNOB_HIST          1 (default): sr_route_pack_many / sr_route_pack_* hand the route kernel's tile
- *                         histograms to the packing; 0: the packing counts the records itself.
+ *                         histograms to the packing; 0: the packing counts the records itself;
+ *   SR_KNOB_PREFETCH      tiles ahead (0 default = off, up to 4096) whose 128-byte lines a route tile
+ *                         workgroup touches after issuing its own loads (an L2 / memory-side cache warm-up
+ *                         for the tile its XCD runs later).
  * Returns 0, -EINVAL (unknown knob or value) or -ENOTSUP. */
 #define SR_KNOB_LB_SPIN 1
 #define SR_KNOB_DEFER_PICKS 2
@@ -419,6 +422,7 @@ int sr_route_pack_trace(sr_ctx *ctx, int slot, const sr_record **records, const 
 #define SR_KNOB_MTU_WALK 5
 #define SR_KNOB_PERSIST 6
 #define SR_KNOB_HIST 7
+#define SR_KNOB_PREFETCH 8
 int sr_set_knob(sr_ctx *ctx, int knob, int64_t value);
 
 /* Page-locked host memory for the batches and outputs of the host-memory calls (their copies then

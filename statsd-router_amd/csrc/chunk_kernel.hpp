@@ -217,6 +217,7 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     if (!(ABL & KV_ALIVE) && p.mark_tiles && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
         sm.img[(uint32_t)tid * 17 + 16] = 0u;
     if (tid == 0) sm.hs[kSlotBefore] = 0ull;
+    const uint32_t pf = prefetch_tile(p, bd, t, tid);
 
     // ---- the chunk: LDS row, '\n' / ':' masks ------------------------------------------------
     uint64_t nlm, clm;
@@ -542,6 +543,7 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         }
     }
     if (tid == 0) arrive(p, blockIdx.x, ep0);
+    prefetch_sink(pf);
     stamp<ABL>(p, tid, g, 9);
 }
 

@@ -77,6 +77,7 @@ struct DeviceState {
     uint64_t *d_cpow = nullptr;          // route_chunk_kernel's power tables (kCpowEntries)
     uint64_t *d_tail = nullptr;          // route_chunk_kernel's tail granules, 4 per tile
     uint32_t lb_spin = 1u << 16;         // its look-back polls before computing a line itself (SR_KNOB_LB_SPIN)
+    uint32_t prefetch = 0;               // SR_KNOB_PREFETCH (RouteParams::prefetch)
     Control *d_ctl = nullptr;
     uint64_t *d_status = nullptr;
     uint64_t *d_bases = nullptr;
@@ -272,6 +273,7 @@ struct DeviceState {
         p.cpow = d_cpow;
         p.tail = d_tail;
         p.lb_spin = lb_spin;
+        p.prefetch = prefetch;
         return p;
     }
 
@@ -490,9 +492,10 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
         hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     }
     if (hipGetLastError() != hipSuccess) return -EIO;
-    // the key histograms exist only where route_kernel counted them with every route final: every shard
-    // alive, or the picks-only probe without deferral (one dead shard: two picks always end it)
-    ds.last_hist = p.hist && (ABL & (KV_ALIVE | KV_PICKS)) && !(ABL & KV_CHUNKS) && !p.defer && ds.dead <= 1;
+    // the key histograms exist only where route_kernel counted them (every shard alive; counting them in
+    // the picks-only variant too, one dead shard, cost that kernel 5 us per C2 launch in SGPR spills:
+    // profiles/r05/hist_one_dead_ab_r5h.jsonl)
+    ds.last_hist = p.hist && (ABL & KV_ALIVE) && !(ABL & KV_CHUNKS);
     if (p.defer || p.mark) {   // the probes past their first two picks and the OR of the tiles' probed-dead
                                // slots (probe_defer_kernel), grid y = batch
         // blocks past a batch's record count return at once; the rest loop over chunks of 4 waves

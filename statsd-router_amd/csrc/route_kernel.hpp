@@ -206,6 +206,11 @@ struct RouteParams {
     uint64_t *tail;
     uint32_t lb_spin;
     uint32_t pworkers;       // route_persist_kernel: workgroups per XCD class (persist_kernel.hpp)
+    // SR_KNOB_PREFETCH (developer A/B): a tile workgroup also touches one dword per 128-byte line of the
+    // tile `prefetch` tiles further on in its batch (the one its XCD runs about that many tiles later),
+    // so that tile's loads find it in L2 / the memory-side cache; 0: off
+    uint32_t prefetch;
+    uint32_t pad_pf;
     // route + pack launches (sr_route_pack_many; every shard alive, at most kHistKeys - 1 shards): per
     // tile its records' key histogram (shard, or nds = unrouted), key-major per batch at
     // hist[(nds + 1) * sbase + key * ntiles + t], for the packing's sort (mtu_kernel.hpp); null: off
@@ -1285,6 +1290,17 @@ __device__ __forceinline__ void tile_issue(const RouteParams &p, uint32_t bi, ui
     }
 }
 
+// SR_KNOB_PREFETCH: one dword of every 128-byte line of tile t + p.prefetch of the batch (the tile
+// this XCD class runs about that many tiles later), issued after the tile's own loads; the value is
+// kept to the workgroup's end (prefetch_sink), so nothing waits for it before then
+__device__ __forceinline__ uint32_t prefetch_tile(const RouteParams &p, const BatchDesc &bd, uint32_t t, int tid) {
+    if (!p.prefetch || tid >= 128 || t + p.prefetch >= bd.ntiles) return 0u;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)bd.nbytes, 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b32(rsrc, (t + p.prefetch) * 16384u + (uint32_t)tid * 128u, 0, 0);
+}
+__device__ __forceinline__ void prefetch_sink(uint32_t v) { asm volatile("" ::"v"(v)); }
+
 // Route one tile (reference: sr-main.c:175-189 + process_data_line + hash + find_downstream's
 // choice, for every line that ends in the tile), in two halves. First half: the tile's bytes from
 // the registers of `in` into the LDS image (thread tid's chunk = image row tid), the '\n' / ':'
@@ -1579,7 +1595,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 }
                 const uint32_t rec = base + (uint32_t)j;
                 if (rec < bd.max_records) {
-                    if constexpr ((ABL & (KV_ALIVE | KV_PICKS)) != 0)   // the packing's key histogram (ds_add, no return)
+                    if constexpr ((ABL & KV_ALIVE) != 0)   // the packing's key histogram (ds_add, no return)
                         if (p.hist) atomicAdd(&sm.hist[route < p.nds ? route : p.nds], 1u);
                     if (deferred) bd.dhash[rec] = h;
                     if (!(ABL & KV_ALIVE) && route == kRoutePending && !deferred) {
@@ -1860,7 +1876,8 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     if (!(ABL & KV_ALIVE) && p.mark_tiles && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
         sm.img[(uint32_t)tid * 17 + 16] = 0u;
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
-    if ((ABL & (KV_ALIVE | KV_PICKS)) && p.hist && tid < kHistKeys) sm.hist[tid] = 0u;
+    if ((ABL & KV_ALIVE) && p.hist && tid < kHistKeys) sm.hist[tid] = 0u;
+    const uint32_t pf = prefetch_tile(p, p.b[bi], t, tid);
     uint64_t nlm, clm;
     uint32_t c_in;
     tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
@@ -1873,12 +1890,13 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
             p.tile_pd[(size_t)(p.b[bi].sbase + t) * p.nwords + tid] = ((uint64_t)hi << 32) | lo;
         }
     }
-    if ((ABL & (KV_ALIVE | KV_PICKS)) && p.hist) {   // the tile's key histogram for the packing (sr_route_pack_many)
+    if ((ABL & KV_ALIVE) && p.hist) {   // the tile's key histogram for the packing (sr_route_pack_many)
         wg_barrier();
         const BatchDesc &bd = p.b[bi];
         if ((uint32_t)tid <= p.nds)
             p.hist[(size_t)(p.nds + 1) * bd.sbase + (size_t)tid * bd.ntiles + t] = sm.hist[tid];
     }
+    prefetch_sink(pf);
     if (tid == 0) arrive(p, blockIdx.x, ep0);
     stamp<ABL>(p, tid, g, 9);
 }

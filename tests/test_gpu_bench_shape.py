@@ -123,6 +123,7 @@ CASES = [
     ("c4", False, 32, "random", True),
     ("c5", False, 32, "random", True),   # 64 shards: the counting pass (no histograms)
     ("c2", True, 32, "random", True),    # dead shards: the counting pass
+    ("c5", True, 32, "random", True),    # 16 of 64 dead (deferred probes)
     ("c2", False, 8, "random"),
     ("c2", False, 9, "random"),
     ("c2", False, 32, "random"),
@@ -262,3 +263,23 @@ def test_route_pack_many_rejects_mismatched_batches(pkg):
         ra[0] = pkg.SrBatch(ok[0], ok[1], ok[2], ok[3], None, ok[5], None)
         pa[0] = pkg.SrPackBatch(bad[2], ok[5], ok[3], ok[7], None, ok[8], ok[9], ok[10], ok[11], ok[12])
         assert pkg.lib().sr_route_pack_many(r.handle, ra, pa, 1) == -22
+
+
+@pytest.mark.parametrize("cfg,layout,dead", [("c2", 1, False), ("c2", 1, True), ("c5", 3, False), ("c5", 3, True),
+                                             ("c4", 2, False)])
+def test_prefetch_knob_same_records(pkg, oracle, cfg, layout, dead):
+    """SR_KNOB_PREFETCH (tiles touched ahead of the route kernel's own loads) changes no output: a
+    9-batch route + pack launch against the oracle, each lane layout, all alive and a quarter dead."""
+    _, _, _, n, _, _ = _cfg(cfg)
+    alive = _alive(cfg, dead)
+    streams = _streams(pkg, cfg, 9)
+    fills = np.random.default_rng(88).integers(0, 1451, (9, n))
+    got, used = _route_pack_many(pkg, streams, n, alive, fills, layout=layout, fused=True,
+                                 knobs=[(pkg.SR_KNOB_PREFETCH, 64)])
+    for b, s in enumerate(streams):
+        recs, cnt, probed = _oracle_route(oracle, cfg, dead, b, s, n, alive)
+        assert got[b]["n_lines"] == cnt, b
+        assert np.array_equal(got[b]["recs"], recs), f"batch {b}: records differ with prefetch"
+        srt_o, pk_o, fo_o, _ = oracle.pack_packets(recs, n, fills[b], probed)
+        assert np.array_equal(got[b]["packets"].view(np.uint8), pk_o.view(np.uint8)), b
+        assert got[b]["fill_out"].tolist() == fo_o.tolist(), b
