@@ -411,9 +411,9 @@ int sr_route_pack_trace(sr_ctx *ctx, int slot, const sr_record **records, const 
  *                         slower: -ENOTSUP otherwise);
  *   SR_KNOB_HIST          1 (default): sr_route_pack_many / sr_route_pack_* hand the route kernel's tile
  *                         histograms to the packing; 0: the packing counts the records itself;
- *   SR_KNOB_PREFETCH      tiles ahead (0 default = off, up to 4096) whose 128-byte lines a route tile
- *                         workgroup touches after issuing its own loads (an L2 / memory-side cache warm-up
- *                         for the tile its XCD runs later).
+ *   SR_KNOB_PREFETCH      tiles ahead (default 64; 0 off; up to 4096) whose 128-byte lines a chunk-layout
+ *                         tile workgroup touches after issuing its own loads (an L2 / memory-side cache
+ *                         warm-up for the tile its XCD runs later).
  * Returns 0, -EINVAL (unknown knob or value) or -ENOTSUP. */
 #define SR_KNOB_LB_SPIN 1
 #define SR_KNOB_DEFER_PICKS 2

@@ -206,9 +206,9 @@ struct RouteParams {
     uint64_t *tail;
     uint32_t lb_spin;
     uint32_t pworkers;       // route_persist_kernel: workgroups per XCD class (persist_kernel.hpp)
-    // SR_KNOB_PREFETCH (developer A/B): a tile workgroup also touches one dword per 128-byte line of the
-    // tile `prefetch` tiles further on in its batch (the one its XCD runs about that many tiles later),
-    // so that tile's loads find it in L2 / the memory-side cache; 0: off
+    // route_chunk_kernel (SR_KNOB_PREFETCH): a tile workgroup also touches one dword per 128-byte line of
+    // the tile `prefetch` tiles further on in its batch (the one its XCD runs about that many tiles
+    // later), so that tile's loads find it in L2 / the memory-side cache; 0: off
     uint32_t prefetch;
     uint32_t pad_pf;
     // route + pack launches (sr_route_pack_many; every shard alive, at most kHistKeys - 1 shards): per
@@ -1290,9 +1290,11 @@ __device__ __forceinline__ void tile_issue(const RouteParams &p, uint32_t bi, ui
     }
 }
 
-// SR_KNOB_PREFETCH: one dword of every 128-byte line of tile t + p.prefetch of the batch (the tile
-// this XCD class runs about that many tiles later), issued after the tile's own loads; the value is
-// kept to the workgroup's end (prefetch_sink), so nothing waits for it before then
+// SR_KNOB_PREFETCH (route_chunk_kernel): one dword of every 128-byte line of tile t + p.prefetch of the
+// batch (the tile this XCD class runs about that many tiles later), issued after the tile's own loads;
+// the value is kept to the workgroup's end (prefetch_sink), so nothing waits for it before then.
+// 64 tiles ahead: C5 169.5 -> 165.4 us per 32-batch launch; 224 (a whole round of resident tiles)
+// +3 %; in route_kernel the code alone cost C2 +4 us (profiles/r05/prefetch_cost_ab_r5j.jsonl)
 __device__ __forceinline__ uint32_t prefetch_tile(const RouteParams &p, const BatchDesc &bd, uint32_t t, int tid) {
     if (!p.prefetch || tid >= 128 || t + p.prefetch >= bd.ntiles) return 0u;
     const __amdgpu_buffer_rsrc_t rsrc =
@@ -1877,7 +1879,6 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
         sm.img[(uint32_t)tid * 17 + 16] = 0u;
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
     if ((ABL & KV_ALIVE) && p.hist && tid < kHistKeys) sm.hist[tid] = 0u;
-    const uint32_t pf = prefetch_tile(p, p.b[bi], t, tid);
     uint64_t nlm, clm;
     uint32_t c_in;
     tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
@@ -1896,7 +1897,6 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
         if ((uint32_t)tid <= p.nds)
             p.hist[(size_t)(p.nds + 1) * bd.sbase + (size_t)tid * bd.ntiles + t] = sm.hist[tid];
     }
-    prefetch_sink(pf);
     if (tid == 0) arrive(p, blockIdx.x, ep0);
     stamp<ABL>(p, tid, g, 9);
 }

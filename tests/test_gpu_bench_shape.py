@@ -265,17 +265,17 @@ def test_route_pack_many_rejects_mismatched_batches(pkg):
         assert pkg.lib().sr_route_pack_many(r.handle, ra, pa, 1) == -22
 
 
-@pytest.mark.parametrize("cfg,layout,dead", [("c2", 1, False), ("c2", 1, True), ("c5", 3, False), ("c5", 3, True),
-                                             ("c4", 2, False)])
-def test_prefetch_knob_same_records(pkg, oracle, cfg, layout, dead):
-    """SR_KNOB_PREFETCH (tiles touched ahead of the route kernel's own loads) changes no output: a
-    9-batch route + pack launch against the oracle, each lane layout, all alive and a quarter dead."""
+@pytest.mark.parametrize("cfg,layout,dead,pf", [("c2", 3, False, 0), ("c5", 3, False, 0), ("c5", 3, True, 224),
+                                                ("c4", 3, False, 224), ("c2", 1, True, 224)])
+def test_prefetch_knob_same_records(pkg, oracle, cfg, layout, dead, pf):
+    """SR_KNOB_PREFETCH (the chunk kernel's touches of tiles ahead of its own loads; default 64) changes no
+    output at other values: a 9-batch route + pack launch against the oracle, all alive and a quarter dead."""
     _, _, _, n, _, _ = _cfg(cfg)
     alive = _alive(cfg, dead)
     streams = _streams(pkg, cfg, 9)
     fills = np.random.default_rng(88).integers(0, 1451, (9, n))
     got, used = _route_pack_many(pkg, streams, n, alive, fills, layout=layout, fused=True,
-                                 knobs=[(pkg.SR_KNOB_PREFETCH, 64)])
+                                 knobs=[(pkg.SR_KNOB_PREFETCH, pf)])
     for b, s in enumerate(streams):
         recs, cnt, probed = _oracle_route(oracle, cfg, dead, b, s, n, alive)
         assert got[b]["n_lines"] == cnt, b
