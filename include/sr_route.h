@@ -411,7 +411,7 @@ int sr_route_pack_trace(sr_ctx *ctx, int slot, const sr_record **records, const 
  *                         slower: -ENOTSUP otherwise);
  *   SR_KNOB_HIST          1 (default): sr_route_pack_many / sr_route_pack_* hand the route kernel's tile
  *                         histograms to the packing; 0: the packing counts the records itself;
- *   SR_KNOB_PREFETCH      tiles ahead (default 64; 0 off; up to 4096) whose 128-byte lines a chunk-layout
+ *   SR_KNOB_PREFETCH      tiles ahead (default 96; 0 off; up to 4096) whose 128-byte lines a chunk-layout
  *                         tile workgroup touches after issuing its own loads (an L2 / memory-side cache
  *                         warm-up for the tile its XCD runs later).
  * Returns 0, -EINVAL (unknown knob or value) or -ENOTSUP. */

@@ -77,7 +77,7 @@ struct DeviceState {
     uint64_t *d_cpow = nullptr;          // route_chunk_kernel's power tables (kCpowEntries)
     uint64_t *d_tail = nullptr;          // route_chunk_kernel's tail granules, 4 per tile
     uint32_t lb_spin = 1u << 16;         // its look-back polls before computing a line itself (SR_KNOB_LB_SPIN)
-    uint32_t prefetch = 64;              // SR_KNOB_PREFETCH (RouteParams::prefetch, chunk layout)
+    uint32_t prefetch = 96;              // SR_KNOB_PREFETCH (RouteParams::prefetch, chunk layout)
     Control *d_ctl = nullptr;
     uint64_t *d_status = nullptr;
     uint64_t *d_bases = nullptr;

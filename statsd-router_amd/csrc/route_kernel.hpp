@@ -1293,8 +1293,9 @@ __device__ __forceinline__ void tile_issue(const RouteParams &p, uint32_t bi, ui
 // SR_KNOB_PREFETCH (route_chunk_kernel): one dword of every 128-byte line of tile t + p.prefetch of the
 // batch (the tile this XCD class runs about that many tiles later), issued after the tile's own loads;
 // the value is kept to the workgroup's end (prefetch_sink), so nothing waits for it before then.
-// 64 tiles ahead: C5 169.5 -> 165.4 us per 32-batch launch; 224 (a whole round of resident tiles)
-// +3 %; in route_kernel the code alone cost C2 +4 us (profiles/r05/prefetch_cost_ab_r5j.jsonl)
+// 64 tiles ahead: C5 169.5 -> 165.4 us per 32-batch launch, 96: 164.6 (16 of 64 dead 201.3-201.6
+// against 203.1-203.7 at 64; profiles/r05/prefetch_distance_r5k.jsonl); 224 (a whole round of
+// resident tiles) +3 %; in route_kernel the code alone cost C2 +4 us (prefetch_cost_ab_r5j.jsonl)
 __device__ __forceinline__ uint32_t prefetch_tile(const RouteParams &p, const BatchDesc &bd, uint32_t t, int tid) {
     if (!p.prefetch || tid >= 128 || t + p.prefetch >= bd.ntiles) return 0u;
     const __amdgpu_buffer_rsrc_t rsrc =
