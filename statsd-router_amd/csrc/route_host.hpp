@@ -274,6 +274,7 @@ struct DeviceState {
         p.tail = d_tail;
         p.lb_spin = lb_spin;
         p.prefetch = prefetch;
+        p.alive_w0 = h_alive ? h_alive[0] : 0ull;
         return p;
     }
 
@@ -474,18 +475,26 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
         hipLaunchKernelGGL((route_persist_kernel<ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     } else
 #endif
+    // KV_DEFER1 (route_kernel.hpp): two or more of at most 64 shards dead, every dead first pick deferred
+    const bool defer1 = !(ABL & KV_ALIVE) && ds.dead >= 2 && ds.dead < ds.nds && ds.nds <= 64 && p.defer &&
+                        p.picks == 1 && !p.mark_tiles;
+    constexpr unsigned kD1 = (ABL & KV_ALIVE) ? ABL : (ABL | KV_DEFER1);
     if constexpr ((ABL & KV_CHUNKS) != 0) {
         static_assert(BLOCK == 256, "route_chunk_kernel: 256 lanes of 64 bytes per 16 KiB tile");
         // its probe stops after the first picks: with two or more dead shards it needs the deferral
         // (no scratch for it, e.g. inside a stream capture: the uniform kernel probes in full)
         if (ds.dead >= 2 && ds.dead < ds.nds && !p.defer)
             hipLaunchKernelGGL((route_kernel<BLOCK, KV_UNIFORM>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
+        else if (defer1)
+            hipLaunchKernelGGL((route_chunk_kernel<kD1>), dim3(p.total_blocks), dim3(256), 0, stream, p);
         else
             hipLaunchKernelGGL((route_chunk_kernel<ABL>), dim3(p.total_blocks), dim3(256), 0, stream, p);
     } else if constexpr ((ABL & KV_PICKS) != 0) {
         // the picks-only variant needs the deferral once two or more shards are dead
         if (ds.dead >= 2 && ds.dead < ds.nds && !p.defer)
             hipLaunchKernelGGL((route_kernel<BLOCK, (ABL & ~KV_PICKS)>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
+        else if (defer1)
+            hipLaunchKernelGGL((route_kernel<BLOCK, kD1>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
         else
             hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     } else {

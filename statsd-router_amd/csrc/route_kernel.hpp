@@ -99,6 +99,12 @@ enum : unsigned {
 // picks always find a live one; two or more: the deferral of probe_defer_kernel) runs a variant
 // with chunk_probe in place of probe_shard, whose 16-entry overlay loop it cannot reach.
 enum : unsigned { KV_UNIFORM = 0u, KV_SEGMENTS = 4194304u, KV_ALIVE = 268435456u, KV_PICKS = 536870912u };
+// KV_DEFER1: the common dead-shard launch, two or more of at most 64 shards dead with every probe that
+// meets a dead shard deferred after one pick (probe_defer_kernel redoes it whole and notes the dead
+// shards it visits): the probe is h % N and one test of the alive word (a kernel argument), with no
+// reciprocal or alive pads in LDS, no marks and no pending list (a variant of the picks-only and
+// chunk kernels).
+constexpr unsigned KV_DEFER1 = 2147483648u;
 
 constexpr uint64_t ipow(uint64_t b, unsigned e) {
     uint64_t r = 1;
@@ -211,6 +217,7 @@ struct RouteParams {
     // later), so that tile's loads find it in L2 / the memory-side cache; 0: off
     uint32_t prefetch;
     uint32_t pad_pf;
+    uint64_t alive_w0;       // KV_DEFER1: the alive bitmap's first word (nds <= 64)
     // route + pack launches (sr_route_pack_many; every shard alive, at most kHistKeys - 1 shards): per
     // tile its records' key histogram (shard, or nds = unrouted), key-major per batch at
     // hist[(nds + 1) * sbase + key * ntiles + t], for the packing's sort (mtu_kernel.hpp); null: off
@@ -732,6 +739,13 @@ __device__ __forceinline__ uint32_t chunk_probe(uint64_t h, const RouteParams &p
         h = (h * 7 + 5) / 3;                                                              // :113
     }
     return kRouteDefer;
+}
+
+// KV_DEFER1's probe (find_downstream's first pick, sr-main.c:98-104): h % N when that shard is alive,
+// else the deferral (probe_defer_kernel runs the whole probe, sr-main.c:86-117)
+__device__ __forceinline__ uint32_t defer1_probe(uint64_t h, const RouteParams &p) {
+    const uint32_t j = mod_magic(h, p.magic_n, p.nds);
+    return ((p.alive_w0 >> j) & 1ull) ? j : kRouteDefer;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1576,6 +1590,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 if (!len_ok) route = SR_ROUTE_INVALID_LENGTH;
                 else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
                 else if (ABL & KV_ALIVE) route = p.nds ? mod_magic(h, p.magic_n, p.nds) : SR_ROUTE_ALL_DEAD;   // :145
+                else if (ABL & KV_DEFER1) route = defer1_probe(h, p);                                // :145
                 else if (ABL & KV_PICKS) route = chunk_probe(h, p, sm.img);                          // :145
                 else route = probe_shard(h, p, nullptr, sm.img, nullptr, p.defer != 0,
                                          p.mark_tiles ? sm.img : nullptr);                          // :145
@@ -1601,7 +1616,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     if constexpr ((ABL & KV_ALIVE) != 0)   // the packing's key histogram (ds_add, no return)
                         if (p.hist) atomicAdd(&sm.hist[route < p.nds ? route : p.nds], 1u);
                     if (deferred) bd.dhash[rec] = h;
-                    if (!(ABL & KV_ALIVE) && route == kRoutePending && !deferred) {
+                    if (!(ABL & (KV_ALIVE | KV_DEFER1)) && route == kRoutePending && !deferred) {
                         const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
                         if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
                     }
@@ -1869,14 +1884,14 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     in.sx = (ABL & ABL_AGENT_GRANULES) ? 0ull
                                        : __hip_atomic_load(&p.ctl->scan_xcc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < S::kPowWords) ((uint32_t *)&sm.kp_lo[0])[tid] = kp;   // kp_lo | kp_hi | kp_inv are contiguous
-    if (!(ABL & KV_ALIVE) && p.dead && p.dead < p.nds && tid < 4 * (int)kMagicLds) {   // the probe's first reciprocals (probe_shard)
+    if (!(ABL & (KV_ALIVE | KV_DEFER1)) && p.dead && p.dead < p.nds && tid < 4 * (int)kMagicLds) {   // the probe's first reciprocals (probe_shard)
         const uint32_t e = (uint32_t)tid >> 2;   // divisor nds - e >= 1: entries e < nds only
         if (e < p.nds) sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)&p.magic[p.nds - e])[tid & 3];
     }
-    if (!(ABL & KV_ALIVE) && p.dead && p.dead < p.nds && p.nds <= 64 * kAliveLds && tid >= (int)kAliveRow0 &&
+    if (!(ABL & (KV_ALIVE | KV_DEFER1)) && p.dead && p.dead < p.nds && p.nds <= 64 * kAliveLds && tid >= (int)kAliveRow0 &&
         (uint32_t)tid < kAliveRow0 + 2 * ((p.nds + 63) / 64))   // the alive words (probe_shard)
         sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)p.alive)[tid - kAliveRow0];
-    if (!(ABL & KV_ALIVE) && p.mark_tiles && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
+    if (!(ABL & (KV_ALIVE | KV_DEFER1)) && p.mark_tiles && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
         sm.img[(uint32_t)tid * 17 + 16] = 0u;
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
     if ((ABL & KV_ALIVE) && p.hist && tid < kHistKeys) sm.hist[tid] = 0u;
@@ -1884,7 +1899,7 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     uint32_t c_in;
     tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
     tile_lines<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
-    if (!(ABL & KV_ALIVE) && p.mark_tiles && p.b[bi].probed_dead) {   // MARK_LDS: the dead shards this tile's probes visited
+    if (!(ABL & (KV_ALIVE | KV_DEFER1)) && p.mark_tiles && p.b[bi].probed_dead) {   // MARK_LDS: the dead shards this tile's probes visited
         wg_barrier();
         if ((uint32_t)tid < p.nwords) {   // the tile's slot, ORed by probe_defer_kernel (no atomics)
             const uint32_t lo = sm.img[(kMarkRow0 + 2 * (uint32_t)tid) * 17 + 16];
