@@ -207,11 +207,11 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     }
     const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t sx = __hip_atomic_load(&p.ctl->scan_xcc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!(ABL & (KV_ALIVE | KV_DEFER1)) && p.dead && p.dead < p.nds && tid < 4 * (int)kMagicLds) {   // probe_shard's first reciprocals
+    if (!(ABL & (KV_ALIVE | KV_DEFER1 | KV_DEAD1)) && p.dead && p.dead < p.nds && tid < 4 * (int)kMagicLds) {   // probe_shard's first reciprocals
         const uint32_t e = (uint32_t)tid >> 2;
         if (e < p.nds) sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)&p.magic[p.nds - e])[tid & 3];
     }
-    if (!(ABL & (KV_ALIVE | KV_DEFER1)) && p.dead && p.dead < p.nds && p.nds <= 64 * kAliveLds && tid >= (int)kAliveRow0 &&
+    if (!(ABL & (KV_ALIVE | KV_DEFER1 | KV_DEAD1)) && p.dead && p.dead < p.nds && p.nds <= 64 * kAliveLds && tid >= (int)kAliveRow0 &&
         (uint32_t)tid < kAliveRow0 + 2 * ((p.nds + 63) / 64))   // the alive words (probe_shard)
         sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)p.alive)[tid - kAliveRow0];
     if (!(ABL & (KV_ALIVE | KV_DEFER1)) && p.mark_tiles && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
@@ -423,13 +423,14 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
         else if (ABL & KV_ALIVE) route = p.nds ? mod_magic(h, p.magic_n, p.nds) : SR_ROUTE_ALL_DEAD;   // :145
         else if (ABL & KV_DEFER1) route = defer1_probe(h, p);   // :145
+        else if (ABL & KV_DEAD1) route = dead1_probe(h, p, sm.img);   // :145
         else route = chunk_probe(h, p, sm.img);   // :145
         const bool deferred = !(ABL & KV_ALIVE) && route == kRouteDefer;
         if (deferred) route = kRoutePending;
         const uint32_t rec = base + (uint32_t)j;
         if (rec < bd.max_records) {
             if (deferred) bd.dhash[rec] = h;
-            if (!(ABL & (KV_ALIVE | KV_DEFER1)) && route == kRoutePending && !deferred) {
+            if (!(ABL & (KV_ALIVE | KV_DEFER1 | KV_DEAD1)) && route == kRoutePending && !deferred) {
                 const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
                 if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
             }

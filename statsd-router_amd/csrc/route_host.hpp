@@ -70,6 +70,8 @@ struct DeviceState {
     uint32_t nds = 0, nwords = 0, dead = 0, max_tiles = 0, pending_cap = 0;
     size_t max_batch = 0;
     Magic magic_n{0, 0, 0};
+    Magic magic_n1{0, 0, 0};             // KV_DEAD1: for h % (nds - 1)
+    uint32_t dead_k = 0;                 // KV_DEAD1: the dead shard when exactly one is
     uint64_t *h_alive = nullptr;
     uint64_t *d_alive = nullptr;
     Magic *d_magic = nullptr;
@@ -143,6 +145,7 @@ struct DeviceState {
                 if (host_div(nn, mg[d]) != nn / d) return -EIO;
         }
         magic_n = n_downstreams ? mg[n_downstreams] : Magic{0, 0, 0};
+        magic_n1 = n_downstreams >= 2 ? mg[n_downstreams - 1] : Magic{0, 0, 0};
         if (hipMemcpy(d_magic, mg.data(), mg.size() * sizeof(Magic), hipMemcpyHostToDevice) != hipSuccess)
             return -EIO;
         std::vector<uint64_t> kp(kPowLo + kPowHi + kPowInv);
@@ -234,6 +237,15 @@ struct DeviceState {
             h_alive[w] = v;
         }
         dead = ndead;
+        dead_k = 0;
+        if (ndead == 1)
+            for (uint32_t w = 0; w < nwords; ++w) {
+                const uint64_t v = h_alive[w] | (w == nwords - 1 && (nds & 63) ? ~0ull << (nds & 63) : 0ull);
+                if (~v) {
+                    dead_k = 64 * w + (uint32_t)__builtin_ctzll(~v);
+                    break;
+                }
+            }
         const bool copied = !nwords || hipMemcpyAsync(d_alive, h_alive, nwords * sizeof(uint64_t),
                                                       hipMemcpyHostToDevice, stream) == hipSuccess;
         // the copy reads h_alive: complete it before the snapshot can change again (also after a
@@ -275,6 +287,8 @@ struct DeviceState {
         p.lb_spin = lb_spin;
         p.prefetch = prefetch;
         p.alive_w0 = h_alive ? h_alive[0] : 0ull;
+        p.magic_n1 = magic_n1;
+        p.dead_k = dead_k;
         return p;
     }
 
@@ -479,6 +493,9 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
     const bool defer1 = !(ABL & KV_ALIVE) && ds.dead >= 2 && ds.dead < ds.nds && ds.nds <= 64 && p.defer &&
                         p.picks == 1 && !p.mark_tiles;
     constexpr unsigned kD1 = (ABL & KV_ALIVE) ? ABL : (ABL | KV_DEFER1);
+    // KV_DEAD1: exactly one dead shard (two picks end every probe)
+    const bool dead1 = !(ABL & KV_ALIVE) && ds.dead == 1 && ds.nds >= 2;
+    constexpr unsigned kK1 = (ABL & KV_ALIVE) ? ABL : (ABL | KV_DEAD1);
     if constexpr ((ABL & KV_CHUNKS) != 0) {
         static_assert(BLOCK == 256, "route_chunk_kernel: 256 lanes of 64 bytes per 16 KiB tile");
         // its probe stops after the first picks: with two or more dead shards it needs the deferral
@@ -487,6 +504,8 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
             hipLaunchKernelGGL((route_kernel<BLOCK, KV_UNIFORM>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
         else if (defer1)
             hipLaunchKernelGGL((route_chunk_kernel<kD1>), dim3(p.total_blocks), dim3(256), 0, stream, p);
+        else if (dead1)
+            hipLaunchKernelGGL((route_chunk_kernel<kK1>), dim3(p.total_blocks), dim3(256), 0, stream, p);
         else
             hipLaunchKernelGGL((route_chunk_kernel<ABL>), dim3(p.total_blocks), dim3(256), 0, stream, p);
     } else if constexpr ((ABL & KV_PICKS) != 0) {
@@ -495,6 +514,8 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
             hipLaunchKernelGGL((route_kernel<BLOCK, (ABL & ~KV_PICKS)>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
         else if (defer1)
             hipLaunchKernelGGL((route_kernel<BLOCK, kD1>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
+        else if (dead1)
+            hipLaunchKernelGGL((route_kernel<BLOCK, kK1>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
         else
             hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     } else {

@@ -105,6 +105,9 @@ enum : unsigned { KV_UNIFORM = 0u, KV_SEGMENTS = 4194304u, KV_ALIVE = 268435456u
 // reciprocal or alive pads in LDS, no marks and no pending list (a variant of the picks-only and
 // chunk kernels).
 constexpr unsigned KV_DEFER1 = 2147483648u;
+// KV_DEAD1: exactly one dead shard (RouteParams::dead_k): find_downstream's two picks in closed form,
+// the second pick's reciprocal a kernel argument (magic_n1), no alive or reciprocal pads in LDS.
+constexpr unsigned KV_DEAD1 = 134217728u;
 
 constexpr uint64_t ipow(uint64_t b, unsigned e) {
     uint64_t r = 1;
@@ -218,6 +221,9 @@ struct RouteParams {
     uint32_t prefetch;
     uint32_t pad_pf;
     uint64_t alive_w0;       // KV_DEFER1: the alive bitmap's first word (nds <= 64)
+    Magic magic_n1;          // KV_DEAD1: for h % (nds - 1)
+    uint32_t dead_k;         // KV_DEAD1: the dead shard
+    uint32_t pad_dk;
     // route + pack launches (sr_route_pack_many; every shard alive, at most kHistKeys - 1 shards): per
     // tile its records' key histogram (shard, or nds = unrouted), key-major per batch at
     // hist[(nds + 1) * sbase + key * ntiles + t], for the packing's sort (mtu_kernel.hpp); null: off
@@ -746,6 +752,19 @@ __device__ __forceinline__ uint32_t chunk_probe(uint64_t h, const RouteParams &p
 __device__ __forceinline__ uint32_t defer1_probe(uint64_t h, const RouteParams &p) {
     const uint32_t j = mod_magic(h, p.magic_n, p.nds);
     return ((p.alive_w0 >> j) & 1ull) ? j : kRouteDefer;
+}
+
+// KV_DEAD1's probe: find_downstream (sr-main.c:86-117) with one dead shard d. The first pick
+// j = h % N (:98) is d only for lines that then zero d's buffer (:106) and swap ds_index[j] with
+// ds_index[N - 1] (:108-111); the second pick h' % (N - 1), h' = (h * 7 + 5) / 3 (:113), lands on
+// ds_index[j] = N - 1 or on an untouched position, and is never d: two picks end every probe.
+__device__ __forceinline__ uint32_t dead1_probe(uint64_t h, const RouteParams &p, uint32_t *img) {
+    const uint32_t n = p.nds, d = p.dead_k;
+    const uint32_t j = mod_magic(h, p.magic_n, n);
+    if (j != d) return j;
+    if (p.mark_tiles) note_dead_lds(img, d);
+    const uint32_t j2 = mod_magic((h * 7 + 5) / 3, p.magic_n1, n - 1);
+    return j2 == j ? n - 1 : j2;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1591,6 +1610,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 else if (!fmt_ok) route = SR_ROUTE_INVALID_FORMAT;
                 else if (ABL & KV_ALIVE) route = p.nds ? mod_magic(h, p.magic_n, p.nds) : SR_ROUTE_ALL_DEAD;   // :145
                 else if (ABL & KV_DEFER1) route = defer1_probe(h, p);                                // :145
+                else if (ABL & KV_DEAD1) route = dead1_probe(h, p, sm.img);                          // :145
                 else if (ABL & KV_PICKS) route = chunk_probe(h, p, sm.img);                          // :145
                 else route = probe_shard(h, p, nullptr, sm.img, nullptr, p.defer != 0,
                                          p.mark_tiles ? sm.img : nullptr);                          // :145
@@ -1616,7 +1636,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                     if constexpr ((ABL & KV_ALIVE) != 0)   // the packing's key histogram (ds_add, no return)
                         if (p.hist) atomicAdd(&sm.hist[route < p.nds ? route : p.nds], 1u);
                     if (deferred) bd.dhash[rec] = h;
-                    if (!(ABL & (KV_ALIVE | KV_DEFER1)) && route == kRoutePending && !deferred) {
+                    if (!(ABL & (KV_ALIVE | KV_DEFER1 | KV_DEAD1)) && route == kRoutePending && !deferred) {
                         const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
                         if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
                     }
@@ -1884,11 +1904,11 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     in.sx = (ABL & ABL_AGENT_GRANULES) ? 0ull
                                        : __hip_atomic_load(&p.ctl->scan_xcc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < S::kPowWords) ((uint32_t *)&sm.kp_lo[0])[tid] = kp;   // kp_lo | kp_hi | kp_inv are contiguous
-    if (!(ABL & (KV_ALIVE | KV_DEFER1)) && p.dead && p.dead < p.nds && tid < 4 * (int)kMagicLds) {   // the probe's first reciprocals (probe_shard)
+    if (!(ABL & (KV_ALIVE | KV_DEFER1 | KV_DEAD1)) && p.dead && p.dead < p.nds && tid < 4 * (int)kMagicLds) {   // the probe's first reciprocals (probe_shard)
         const uint32_t e = (uint32_t)tid >> 2;   // divisor nds - e >= 1: entries e < nds only
         if (e < p.nds) sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)&p.magic[p.nds - e])[tid & 3];
     }
-    if (!(ABL & (KV_ALIVE | KV_DEFER1)) && p.dead && p.dead < p.nds && p.nds <= 64 * kAliveLds && tid >= (int)kAliveRow0 &&
+    if (!(ABL & (KV_ALIVE | KV_DEFER1 | KV_DEAD1)) && p.dead && p.dead < p.nds && p.nds <= 64 * kAliveLds && tid >= (int)kAliveRow0 &&
         (uint32_t)tid < kAliveRow0 + 2 * ((p.nds + 63) / 64))   // the alive words (probe_shard)
         sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)p.alive)[tid - kAliveRow0];
     if (!(ABL & (KV_ALIVE | KV_DEFER1)) && p.mark_tiles && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet

@@ -283,3 +283,26 @@ def test_prefetch_knob_same_records(pkg, oracle, cfg, layout, dead, pf):
         srt_o, pk_o, fo_o, _ = oracle.pack_packets(recs, n, fills[b], probed)
         assert np.array_equal(got[b]["packets"].view(np.uint8), pk_o.view(np.uint8)), b
         assert got[b]["fill_out"].tolist() == fo_o.tolist(), b
+
+
+@pytest.mark.parametrize("cfg,layout,dead_k", [("c5", 3, 0), ("c5", 3, 63), ("c5", 3, 17), ("c2", 1, 3), ("c2", 1, 0),
+                                               ("c4", 2, 15), ("c2", 3, 2)])
+def test_exactly_one_dead_shard(pkg, oracle, cfg, layout, dead_k):
+    """Exactly one dead shard (KV_DEAD1: find_downstream's two picks in closed form), the last shard, the
+    first and one inside, in each lane layout: a 9-batch route + pack launch against the oracle, records,
+    probed-dead bitmaps, packets and pending bytes."""
+    _, _, _, n, _, _ = _cfg(cfg)
+    alive = [0 if k == dead_k else 1 for k in range(n)]
+    streams = _streams(pkg, cfg, 9)
+    fills = np.random.default_rng(300 + dead_k).integers(0, 1451, (9, n))
+    got, used = _route_pack_many(pkg, streams, n, alive, fills, layout=layout, fused=True)
+    assert used == layout
+    for b, s in enumerate(streams):
+        recs, _, cnt = oracle.route(s.data, n, alive)
+        probed = oracle.probed_dead(s.data, n, alive)
+        assert got[b]["n_lines"] == cnt, b
+        assert np.array_equal(got[b]["recs"], recs), f"batch {b}: records differ"
+        assert got[b]["probed"].tolist() == probed.tolist(), b
+        srt_o, pk_o, fo_o, _ = oracle.pack_packets(recs, n, fills[b], probed)
+        assert np.array_equal(got[b]["packets"].view(np.uint8), pk_o.view(np.uint8)), b
+        assert got[b]["fill_out"].tolist() == fo_o.tolist(), b
