@@ -514,6 +514,8 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
             hipLaunchKernelGGL((route_kernel<BLOCK, (ABL & ~KV_PICKS)>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
         else if (defer1)
             hipLaunchKernelGGL((route_kernel<BLOCK, kD1>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
+        else if (dead1 && p.hist)
+            hipLaunchKernelGGL((route_kernel<BLOCK, kK1 | KV_HIST1>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
         else if (dead1)
             hipLaunchKernelGGL((route_kernel<BLOCK, kK1>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
         else
@@ -522,10 +524,10 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
         hipLaunchKernelGGL((route_kernel<BLOCK, ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     }
     if (hipGetLastError() != hipSuccess) return -EIO;
-    // the key histograms exist only where route_kernel counted them (every shard alive; counting them in
-    // the picks-only variant too, one dead shard, cost that kernel 5 us per C2 launch in SGPR spills:
-    // profiles/r05/hist_one_dead_ab_r5h.jsonl)
-    ds.last_hist = p.hist && (ABL & KV_ALIVE) && !(ABL & KV_CHUNKS);
+    // the key histograms exist only where route_kernel counted them: every shard alive, or exactly one
+    // dead (KV_DEAD1: two picks end every probe in the kernel). (Counting them in the general picks-only
+    // variant cost it 5 us per C2 launch in SGPR spills: profiles/r05/hist_one_dead_ab_r5h.jsonl.)
+    ds.last_hist = p.hist && !(ABL & KV_CHUNKS) && ((ABL & KV_ALIVE) || ((ABL & KV_PICKS) && dead1));
     if (p.defer || p.mark) {   // the probes past their first two picks and the OR of the tiles' probed-dead
                                // slots (probe_defer_kernel), grid y = batch
         // blocks past a batch's record count return at once; the rest loop over chunks of 4 waves

@@ -108,6 +108,12 @@ constexpr unsigned KV_DEFER1 = 2147483648u;
 // KV_DEAD1: exactly one dead shard (RouteParams::dead_k): find_downstream's two picks in closed form,
 // the second pick's reciprocal a kernel argument (magic_n1), no alive or reciprocal pads in LDS.
 constexpr unsigned KV_DEAD1 = 134217728u;
+// KV_HIST1: the KV_DEAD1 uniform / segment variant that also counts the tile histograms of a route + pack
+// launch (RouteParams::hist); a variant of its own because the counting costs the route-only variant
+// 3 % in SGPR spills (every-shard-alive variants count them at no cost)
+constexpr unsigned KV_HIST1 = 1048576u;
+template <unsigned ABL>
+constexpr bool kCountsHist = (ABL & KV_ALIVE) != 0 || ((ABL & KV_DEAD1) != 0 && (ABL & KV_HIST1) != 0);
 
 constexpr uint64_t ipow(uint64_t b, unsigned e) {
     uint64_t r = 1;
@@ -1633,7 +1639,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                 }
                 const uint32_t rec = base + (uint32_t)j;
                 if (rec < bd.max_records) {
-                    if constexpr ((ABL & KV_ALIVE) != 0)   // the packing's key histogram (ds_add, no return)
+                    if constexpr (kCountsHist<ABL>)   // the packing's key histogram (ds_add, no return)
                         if (p.hist) atomicAdd(&sm.hist[route < p.nds ? route : p.nds], 1u);
                     if (deferred) bd.dhash[rec] = h;
                     if (!(ABL & (KV_ALIVE | KV_DEFER1 | KV_DEAD1)) && route == kRoutePending && !deferred) {
@@ -1914,7 +1920,7 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     if (!(ABL & (KV_ALIVE | KV_DEFER1)) && p.mark_tiles && tid >= (int)kMarkRow0 && (uint32_t)tid < kMarkRow0 + 2 * p.nwords)   // MARK_LDS: none yet
         sm.img[(uint32_t)tid * 17 + 16] = 0u;
     if (tid < 20) sm.img[S::kRows * 17 + tid] = 0u;
-    if ((ABL & KV_ALIVE) && p.hist && tid < kHistKeys) sm.hist[tid] = 0u;
+    if (kCountsHist<ABL> && p.hist && tid < kHistKeys) sm.hist[tid] = 0u;
     uint64_t nlm, clm;
     uint32_t c_in;
     tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
@@ -1927,7 +1933,7 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
             p.tile_pd[(size_t)(p.b[bi].sbase + t) * p.nwords + tid] = ((uint64_t)hi << 32) | lo;
         }
     }
-    if ((ABL & KV_ALIVE) && p.hist) {   // the tile's key histogram for the packing (sr_route_pack_many)
+    if (kCountsHist<ABL> && p.hist) {   // the tile's key histogram for the packing (sr_route_pack_many)
         wg_barrier();
         const BatchDesc &bd = p.b[bi];
         if ((uint32_t)tid <= p.nds)

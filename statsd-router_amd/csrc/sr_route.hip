@@ -674,7 +674,8 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
     return pack_many_impl(c, batches, count, nullptr, nullptr);
 }
 
-// Route (one launch) and pack. With every shard alive and at most kHistKeys - 1 shards the route
+// Route (one launch) and pack. With every shard alive (or exactly one dead: KV_DEAD1) and at most
+// kHistKeys - 1 shards the route
 // kernel (uniform / segment layouts) also writes each tile's key histogram and the packing skips
 // mtu_count, its own pass over the records: C2 packing 0.118-0.120 -> 0.108-0.114 ms, C3 0.075-0.077
 // -> 0.069-0.071 per 32 batches. Batches whose record capacity says fewer than 32 lines per 16 KiB
@@ -683,7 +684,7 @@ int sr_pack_packets_many(sr_ctx *c, const sr_pack_batch *batches, size_t count) 
 // profiles/r05/pack_hist_ab_r5e.jsonl).
 static int route_pack_impl(sr_ctx *c, const sr_batch *route, const sr_pack_batch *pack, size_t count) {
     DeviceState &ds = c->ds;
-    bool want = c->hist && ds.dead == 0 && ds.nds >= 1 && ds.nds < (uint32_t)kHistKeys;
+    bool want = c->hist && ds.dead <= 1 && ds.nds >= 1 && ds.nds < (uint32_t)kHistKeys;
     for (size_t i = 0; want && i < count; ++i)
         want = route[i].max_records * 512 >= route[i].nbytes;
     if (want && !ds.d_hist) {
