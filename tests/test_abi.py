@@ -119,8 +119,10 @@ def test_product_library_has_only_the_product_route_kernels(pkg):
     """Ablation variants (some write wrong records by design) never ship: the product library holds
     exactly the three lane layouts, KV_UNIFORM (0), KV_SEGMENTS (4194304) and KV_CHUNKS (8388608,
     route_chunk_kernel), each also as KV_ALIVE (+268435456: launches with every shard alive), the
-    first two also as KV_PICKS (+536870912: probes that end after their first picks), which write
-    identical records (tests/test_gpu_layout.py); ablations live in tools/ and
+    first two also as KV_PICKS (+536870912: probes that end after their first picks), and the dead-shard
+    specialisations KV_DEFER1 (+2147483648: one pick, then the deferral) and KV_DEAD1 (+134217728:
+    exactly one dead shard; with KV_HIST1, +1048576, for route + pack launches), which write identical
+    records (tests/test_gpu_layout.py, tests/test_gpu_bench_shape.py); ablations live in tools/ and
     `make VARIANTS=1` builds only."""
     out = subprocess.run(["nm", "-C", pkg.ROUTE_LIB], capture_output=True, text=True).stdout
     kernels = {l.split(" ", 2)[-1] for l in out.splitlines()
@@ -131,6 +133,14 @@ def test_product_library_has_only_the_product_route_kernels(pkg):
                        "void srk::route_kernel<256, 272629760u>(srk::RouteParams)",     # KV_SEGMENTS | KV_ALIVE
                        "void srk::route_kernel<256, 536870912u>(srk::RouteParams)",     # KV_PICKS
                        "void srk::route_kernel<256, 541065216u>(srk::RouteParams)",     # KV_SEGMENTS | KV_PICKS
+                       "void srk::route_kernel<256, 2684354560u>(srk::RouteParams)",    # KV_PICKS | KV_DEFER1
+                       "void srk::route_kernel<256, 2688548864u>(srk::RouteParams)",    # KV_SEGMENTS | KV_PICKS | KV_DEFER1
+                       "void srk::route_kernel<256, 671088640u>(srk::RouteParams)",     # KV_PICKS | KV_DEAD1
+                       "void srk::route_kernel<256, 675282944u>(srk::RouteParams)",     # KV_SEGMENTS | KV_PICKS | KV_DEAD1
+                       "void srk::route_kernel<256, 672137216u>(srk::RouteParams)",     # ... | KV_HIST1
+                       "void srk::route_kernel<256, 676331520u>(srk::RouteParams)",     # KV_SEGMENTS ... | KV_HIST1
                        "void srk::route_chunk_kernel<8388608u>(srk::RouteParams)",
-                       "void srk::route_chunk_kernel<276824064u>(srk::RouteParams)"}, kernels   # | KV_ALIVE
+                       "void srk::route_chunk_kernel<276824064u>(srk::RouteParams)",    # | KV_ALIVE
+                       "void srk::route_chunk_kernel<2155872256u>(srk::RouteParams)",   # | KV_DEFER1
+                       "void srk::route_chunk_kernel<142606336u>(srk::RouteParams)"}, kernels   # | KV_DEAD1
     assert b"SR_VARIANT" not in open(pkg.ROUTE_LIB, "rb").read()
