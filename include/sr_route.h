@@ -413,7 +413,10 @@ int sr_route_pack_trace(sr_ctx *ctx, int slot, const sr_record **records, const 
  *                         histograms to the packing; 0: the packing counts the records itself;
  *   SR_KNOB_PREFETCH      tiles ahead (default 96; 0 off; up to 4096) whose 128-byte lines a chunk-layout
  *                         tile workgroup touches after issuing its own loads (an L2 / memory-side cache
- *                         warm-up for the tile its XCD runs later).
+ *                         warm-up for the tile its XCD runs later);
+ *   SR_KNOB_FUSE_DEFER    1: a route + pack launch with two or more (at most 16) dead shards leaves its
+ *                         deferred probes to the packing's counting pass; 0 (default): probe_defer_kernel
+ *                         (measured level on C3 / C5, slower on C4).
  * Returns 0, -EINVAL (unknown knob or value) or -ENOTSUP. */
 #define SR_KNOB_LB_SPIN 1
 #define SR_KNOB_DEFER_PICKS 2
@@ -423,6 +426,7 @@ int sr_route_pack_trace(sr_ctx *ctx, int slot, const sr_record **records, const 
 #define SR_KNOB_PERSIST 6
 #define SR_KNOB_HIST 7
 #define SR_KNOB_PREFETCH 8
+#define SR_KNOB_FUSE_DEFER 9
 int sr_set_knob(sr_ctx *ctx, int knob, int64_t value);
 
 /* Page-locked host memory for the batches and outputs of the host-memory calls (their copies then

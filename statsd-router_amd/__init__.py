@@ -60,7 +60,7 @@ SR_LAYOUT_AUTO, SR_LAYOUT_UNIFORM, SR_LAYOUT_SEGMENTS, SR_LAYOUT_CHUNKS = 0, 1, 
 SR_COMM_ID_BYTES = 128
 # sr_set_knob (developer / test knobs of one context; none changes a result)
 SR_KNOB_LB_SPIN, SR_KNOB_DEFER_PICKS, SR_KNOB_MTU_CHUNK, SR_KNOB_MTU_XCD, SR_KNOB_MTU_WALK, SR_KNOB_PERSIST = 1, 2, 3, 4, 5, 6
-SR_KNOB_HIST, SR_KNOB_PREFETCH = 7, 8
+SR_KNOB_HIST, SR_KNOB_PREFETCH, SR_KNOB_FUSE_DEFER = 7, 8, 9
 LAYOUT_NAMES = {0: "none", 1: "uniform", 2: "segments", 3: "chunks"}
 PACKET_DTYPE = np.dtype([("first", "<u4"), ("nlines", "<u2"), ("shard", "<u2"), ("length", "<u2"),
                          ("carry", "<u2"), ("open", "<u4")])

@@ -96,6 +96,7 @@ struct MtuBatchArg {
     uint32_t tile0;                // first record tile of the batch in the launch's scratch
     uint32_t chunk0;               // first chunk of the batch in the launch's scratch
     uint32_t grp0;                 // group mode: the batch's first scatter group in the launch
+    const uint64_t *dhash;         // fused deferral: the route launch's deferred hashes, by record index
 };
 
 struct MtuLaunch {
@@ -118,6 +119,12 @@ struct MtuLaunch {
     // histograms it wrote (RouteParams::hist, = tile_counts); the scatter's wave takes `group` of
     // them (0: the classic 1024-record tiles of mtu_count)
     uint32_t group, groups;
+    // fused deferral (sr_route_pack_many / sr_route_pack_*, two or more dead shards): the route launch
+    // left its deferred probes pending (no probe_defer_kernel); mtu_count_kernel<true> runs them whole
+    // (find_downstream, sr-main.c:86-117), writes their routes back and notes the dead shards they visit
+    // in the batches' probed-dead bitmaps (fd_mark) before counting
+    ProbeArgs probe;
+    uint32_t fd_mark, nwords;
     MtuBatchArg b[kMtuMaxBatches];
 };
 static_assert(sizeof(MtuLaunch) < 3584, "kernel argument size");
@@ -252,10 +259,68 @@ __device__ __forceinline__ void mtu_wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
+// FD: the fused deferral (MtuLaunch::probe). The wave lists its tile's pending records in LDS
+// (ballots, as probe_defer_kernel), every lane probes list entries (pads of reciprocals and alive
+// words in LDS, the dead shards visited in the wave's LDS words, ORed into the batch's bitmap at
+// the end), writes the route back into the record and counts it; the other records are counted by
+// their own lanes.
+template <bool FD>
 __global__ __launch_bounds__(64 * kMtuSortWaves) void mtu_count_kernel(MtuLaunch L) {
     extern __shared__ uint32_t lds_hist[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t g = blockIdx.x * kMtuSortWaves + (uint32_t)wave;   // the wave's tile in the launch
+    if constexpr (FD) {
+        __shared__ uint32_t pads[kProbePads];
+        __shared__ uint32_t plist[kMtuSortWaves][kMtuTile];
+        __shared__ unsigned long long wgm[kMtuSortWaves][kReplayCheckWords];
+        uint32_t pv;
+        if (probe_pad_value(L.probe, threadIdx.x, pv)) pads[threadIdx.x * 17 + 16] = pv;
+        if (lane < (int)kReplayCheckWords) wgm[wave][lane] = 0ull;
+        __syncthreads();
+        if (g >= L.tiles) return;
+        const uint32_t bi = mtu_batch_of(L, g, [](const MtuBatchArg &a) { return a.tile0; });
+        const MtuParams p = mtu_view(L, bi);
+        const uint32_t nk = p.nds + 1, t = g - L.b[bi].tile0;
+        uint32_t *hist = lds_hist + (size_t)wave * nk;
+        const uint32_t n = mtu_lines(p), r0 = t * kMtuTile;
+        sr_record r[kMtuPerLane];
+        if (r0 < n) mtu_load_tile(p, r0, n, lane, r);
+        for (uint32_t k = lane; k < nk; k += 64) hist[k] = 0;
+        mtu_wave_sync();
+        if (r0 >= n) {
+            for (uint32_t k = lane; k < nk; k += 64) p.tile_counts[(size_t)k * p.ntiles + t] = 0u;
+            return;
+        }
+        const uint64_t below = (1ull << lane) - 1ull;
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int k = 0; k < kMtuPerLane; ++k) {
+            const uint32_t i = r0 + (uint32_t)(64 * k + lane);
+            const bool valid = i < n;
+            const bool pend = valid && r[k].route == kRoutePending;
+            const uint64_t m = __ballot(pend);
+            if (pend) plist[wave][cnt + (uint32_t)__popcll(m & below)] = i;
+            cnt += (uint32_t)__popcll(m);
+            if (valid && !pend) atomicAdd(&hist[mtu_key(r[k], p.nds)], 1u);
+        }
+        mtu_wave_sync();
+        uint64_t *const mark = L.fd_mark ? const_cast<uint64_t *>(p.probed_dead) : nullptr;
+        sr_record *const recs = const_cast<sr_record *>(p.recs);
+        const uint64_t *const dh = L.b[bi].dhash;
+        for (uint32_t j = (uint32_t)lane; j < cnt; j += 64u) {
+            const uint32_t x = plist[wave][j];
+            const uint64_t h = dh[x];
+            const uint32_t route = mark ? probe_shard<true>(h, L.probe, mark, pads, wgm[wave])
+                                        : probe_shard(h, L.probe, nullptr, pads);
+            recs[x].route = (uint16_t)route;
+            atomicAdd(&hist[route < p.nds ? route : p.nds], 1u);
+        }
+        mtu_wave_sync();
+        for (uint32_t k = lane; k < nk; k += 64) p.tile_counts[(size_t)k * p.ntiles + t] = hist[k];
+        if (mark && (uint32_t)lane < L.nwords && wgm[wave][lane])
+            __hip_atomic_fetch_or(mark + lane, (uint64_t)wgm[wave][lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
     if (g >= L.tiles) return;
     const uint32_t bi = mtu_batch_of(L, g, [](const MtuBatchArg &a) { return a.tile0; });
     const MtuParams p = mtu_view(L, bi);

@@ -106,6 +106,11 @@ struct DeviceState {
     uint32_t persist = 0;
     uint32_t *d_hist = nullptr;      // RouteParams::hist (sr_route_pack_many), max_tiles x kHistKeys
     bool last_hist = false;          // the last launch wrote its tiles' key histograms
+    // fused deferral (route + pack launches, SR_KNOB_FUSE_DEFER, off by default): asked for by the caller, and whether
+    // the last launch left its deferred probes to the packing's counting pass (mtu_count_kernel<true>)
+    bool fuse_defer = false, last_fused = false;
+    uint32_t fd_mark = 0;
+    const uint64_t *fd_dhash[kMaxBatches] = {};
     uint32_t persist_slots = 0;      // resident route_persist_kernel workgroups on the device (0: not yet asked)
 
     int init(size_t max_batch_bytes, uint32_t n_downstreams) {
@@ -489,6 +494,15 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
         hipLaunchKernelGGL((route_persist_kernel<ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
     } else
 #endif
+    // Route + pack with every dead first pick deferred and at most kOverlay dead (no wide probes), at most
+    // 1024 shards: the packing's counting pass runs the deferred probes (no probe_defer_kernel)
+    const bool fused = ds.fuse_defer && p.defer && p.picks == 1 && !p.mark_tiles && ds.dead <= (uint32_t)kOverlay &&
+                       ds.nwords <= kReplayCheckWords && (p.mark || !replay);
+    ds.last_fused = fused;
+    if (fused) {
+        ds.fd_mark = p.mark;
+        for (uint32_t j = 0; j < p.nb; ++j) ds.fd_dhash[j] = p.b[j].dhash;
+    }
     // KV_DEFER1 (route_kernel.hpp): two or more of at most 64 shards dead, every dead first pick deferred
     const bool defer1 = !(ABL & KV_ALIVE) && ds.dead >= 2 && ds.dead < ds.nds && ds.nds <= 64 && p.defer &&
                         p.picks == 1 && !p.mark_tiles;
@@ -528,7 +542,7 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
     // dead (KV_DEAD1: two picks end every probe in the kernel). (Counting them in the general picks-only
     // variant cost it 5 us per C2 launch in SGPR spills: profiles/r05/hist_one_dead_ab_r5h.jsonl.)
     ds.last_hist = p.hist && !(ABL & KV_CHUNKS) && ((ABL & KV_ALIVE) || ((ABL & KV_PICKS) && dead1));
-    if (p.defer || p.mark) {   // the probes past their first two picks and the OR of the tiles' probed-dead
+    if ((p.defer || p.mark) && !fused) {   // the probes past their first two picks and the OR of the tiles' probed-dead
                                // slots (probe_defer_kernel), grid y = batch
         // blocks past a batch's record count return at once; the rest loop over chunks of 4 waves
         const uint32_t bx = p.defer ? (max_recs + 4u * kDeferChunk - 1u) / (4u * kDeferChunk) : 1u;

@@ -649,8 +649,16 @@ __device__ __forceinline__ void note_dead_wg(uint64_t *pd, unsigned long long *w
 // DEFER (the route kernel, with dead shards): a line still unresolved after its first two picks
 // returns kRouteDefer; probe_defer_kernel runs its whole probe later, one lane per line (a wave
 // that runs the overlay loop below for one of its lines holds all its lanes for every step).
-template <bool MARK = false>
-__device__ uint32_t probe_shard(uint64_t h, const RouteParams &p, uint64_t *mark = nullptr,
+// What probe_shard reads of its parameters (RouteParams, or ProbeArgs in the packing's counting pass)
+struct ProbeArgs {
+    uint32_t nds, dead, picks, pad;
+    Magic magic_n;
+    const uint64_t *alive;
+    const Magic *magic;
+};
+
+template <bool MARK = false, class P = RouteParams>
+__device__ uint32_t probe_shard(uint64_t h, const P &p, uint64_t *mark = nullptr,
                                 const uint32_t *pad_img = nullptr, unsigned long long *mark_wg = nullptr,
                                 bool defer = false, uint32_t *mark_lds = nullptr) {
     const uint32_t n = p.nds;
@@ -1955,7 +1963,8 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
 // (magic_from_pad, alive_pad_dword), for the kernels after it: a probe step then waits on LDS, not
 // on a dependent global load per step.
 constexpr uint32_t kProbePads = (kAliveRow0 + 2 * kAliveLds) * 17;
-__device__ __forceinline__ bool probe_pad_value(const RouteParams &p, uint32_t tid, uint32_t &v) {
+template <class P>
+__device__ __forceinline__ bool probe_pad_value(const P &p, uint32_t tid, uint32_t &v) {
     if (tid < 4 * kMagicLds && (tid >> 2) < p.nds) {
         v = ((const uint32_t *)&p.magic[p.nds - (tid >> 2)])[tid & 3];
         return true;

@@ -65,6 +65,7 @@ struct sr_ctx {
     uint32_t mtu_chunk;
     int mtu_xcd, mtu_walk;
     int hist;                     // SR_KNOB_HIST: route + pack launches hand the tiles' histograms over
+    int fuse_defer;               // SR_KNOB_FUSE_DEFER: the counting pass runs the route launch's deferred probes
     // page-locked, device-mapped outputs of sr_route_pack_submit: slots 0 and 1, slot 2 is
     // sr_route_pack_batch's own
     struct Slot {
@@ -222,6 +223,7 @@ int sr_open(sr_ctx **out, int device, size_t max_batch_bytes, uint32_t n_downstr
     c->mtu_xcd = 1;
     c->mtu_walk = 1;
     c->hist = 1;
+    c->fuse_defer = 0;   // measured level or slower (C4: too few counting waves): profiles/r05/fused_deferral_ab_r5r.jsonl
     int rc = -ENOMEM;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) goto fail;
     c->stream = c->own_stream;
@@ -264,6 +266,10 @@ int sr_set_knob(sr_ctx *c, int knob, int64_t v) {
     case SR_KNOB_LB_SPIN:
         if (v < 0 || v > 0xFFFFFFFFll) return -EINVAL;
         c->ds.lb_spin = (uint32_t)v;
+        return 0;
+    case SR_KNOB_FUSE_DEFER:
+        if (v != 0 && v != 1) return -EINVAL;
+        c->fuse_defer = (int)v;
         return 0;
     case SR_KNOB_PREFETCH:
         if (v < 0 || v > 4096) return -EINVAL;
@@ -536,7 +542,7 @@ extern "C" size_t sr_mtu_stamps(uint64_t *dst, size_t max_chunks) {
 // context's last route launch (RouteParams::hist); route_bytes: each batch's bytes in that launch
 // (its tiles: ceil(bytes / 16 KiB), numbered in batch order as launch_route numbers them)
 static int pack_many_impl(sr_ctx *c, const sr_pack_batch *batches, size_t count, uint32_t *hist,
-                          const size_t *route_bytes) {
+                          const size_t *route_bytes, bool fused = false) {
     if (!c || !batches || count == 0 || count > (size_t)kMtuMaxBatches) return -EINVAL;
     const uint32_t nds = c->ds.nds;
     if (nds > SR_MAX_PACK_DOWNSTREAMS) return -EINVAL;
@@ -602,6 +608,14 @@ static int pack_many_impl(sr_ctx *c, const sr_pack_batch *batches, size_t count,
     L.nx = reinterpret_cast<uint8_t *>(c->d_mtu_table + (((size_t)c->mtu_chunks * kMtuX + 1) & ~(size_t)1));
     L.plen = reinterpret_cast<uint16_t *>(c->d_mtu_gp);
     L.gp0 = c->d_mtu_gp + (size_t)c->mtu_chunks * kMtuChunk / 2;
+    if (fused) {   // the route launch's deferred probes, run by the counting pass
+        if (hist) return -EIO;
+        const DeviceState &ds = c->ds;
+        L.probe = ProbeArgs{ds.nds, ds.dead, 2u, 0u, ds.magic_n, ds.d_alive, ds.d_magic};
+        L.fd_mark = ds.fd_mark;
+        L.nwords = ds.nwords;
+        for (size_t j = 0; j < count; ++j) L.b[j].dhash = ds.fd_dhash[j];
+    }
 #ifdef SR_MTU_STAMPS   // developer timeline: 8 stamps per chunk, read back with sr_mtu_stamps
     static uint64_t *d_dbg = nullptr;
     static size_t dbg_cap = 0;
@@ -632,7 +646,8 @@ static int pack_many_impl(sr_ctx *c, const sr_pack_batch *batches, size_t count,
     }
     const size_t sort_lds = (size_t)kMtuSortWaves * (nds + 1) * sizeof(uint32_t);
     // up to 4 x 4097 counters: past the 64 KiB default
-    ensure_dyn_lds((const void *)mtu_count_kernel, 96 * 1024);
+    ensure_dyn_lds((const void *)mtu_count_kernel<false>, 96 * 1024);
+    ensure_dyn_lds((const void *)mtu_count_kernel<true>, 64 * 1024);
     ensure_dyn_lds((const void *)mtu_scatter_kernel, 96 * 1024);
     if (hist) {   // the route kernel counted the keys: scan its tiles' histograms, scatter by groups of tiles
         ensure_dyn_lds((const void *)mtu_scatter_groups_kernel, 96 * 1024);
@@ -642,7 +657,10 @@ static int pack_many_impl(sr_ctx *c, const sr_pack_batch *batches, size_t count,
             hipLaunchKernelGGL(mtu_scatter_groups_kernel, dim3(gblocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
     } else {
         const uint32_t sort_blocks = (tiles + kMtuSortWaves - 1) / kMtuSortWaves;
-        hipLaunchKernelGGL(mtu_count_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
+        if (fused)
+            hipLaunchKernelGGL(mtu_count_kernel<true>, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
+        else
+            hipLaunchKernelGGL(mtu_count_kernel<false>, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
         hipLaunchKernelGGL(mtu_scan_kernel, dim3((uint32_t)count), dim3(1024), 0, c->stream, L);
         hipLaunchKernelGGL(mtu_scatter_kernel, dim3(sort_blocks), dim3(64 * kMtuSortWaves), sort_lds, c->stream, L);
     }
@@ -700,9 +718,13 @@ static int route_pack_impl(sr_ctx *c, const sr_batch *route, const sr_pack_batch
     }
     p.hist = want ? ds.d_hist : nullptr;
     ds.last_hist = false;
+    ds.fuse_defer = c->fuse_defer && !want;
     int rc = launch_variant(ds, p, c->stream);
+    ds.fuse_defer = false;
     if (rc) return rc;
-    return pack_many_impl(c, pack, count, ds.last_hist ? ds.d_hist : nullptr, bytes);
+    const bool fused = ds.last_fused;
+    ds.last_fused = false;
+    return pack_many_impl(c, pack, count, ds.last_hist ? ds.d_hist : nullptr, bytes, fused);
 }
 
 int sr_route_pack_many(sr_ctx *c, const sr_batch *route, const sr_pack_batch *pack, size_t count) {

@@ -306,3 +306,29 @@ def test_exactly_one_dead_shard(pkg, oracle, cfg, layout, dead_k):
         srt_o, pk_o, fo_o, _ = oracle.pack_packets(recs, n, fills[b], probed)
         assert np.array_equal(got[b]["packets"].view(np.uint8), pk_o.view(np.uint8)), b
         assert got[b]["fill_out"].tolist() == fo_o.tolist(), b
+
+
+@pytest.mark.parametrize("cfg,n_dead,fuse", [("c4", 7, 1), ("c5", 16, 1), ("c5", 17, 1), ("c3", 2, 1), ("c5", 16, 0),
+                                             ("c5", 3, 1)])
+def test_fused_deferral(pkg, oracle, cfg, n_dead, fuse):
+    """Route + pack with two or more dead shards: the packing's counting pass runs the route launch's
+    deferred probes (SR_KNOB_FUSE_DEFER 1, up to 16 dead; 17 falls back to probe_defer_kernel and the
+    wide probe), against the oracle: records (routes written back), probed-dead bitmaps, packets."""
+    _, _, _, n, _, _ = _cfg(cfg)
+    rng = np.random.default_rng(500 + n_dead)
+    dead = set(rng.choice(n, n_dead, replace=False).tolist())
+    alive = [0 if k in dead else 1 for k in range(n)]
+    streams = _streams(pkg, cfg, 9)
+    fills = rng.integers(0, 1451, (9, n))
+    got, _ = _route_pack_many(pkg, streams, n, alive, fills, fused=True, knobs=[(pkg.SR_KNOB_FUSE_DEFER, fuse)])
+    for b, s in enumerate(streams):
+        recs, _, cnt = oracle.route(s.data, n, alive)
+        probed = oracle.probed_dead(s.data, n, alive)
+        assert got[b]["n_lines"] == cnt, b
+        assert np.array_equal(got[b]["recs"], recs), f"batch {b}: records differ"
+        assert got[b]["probed"].tolist() == probed.tolist(), b
+        srt_o, pk_o, fo_o, nv_o = oracle.pack_packets(recs, n, fills[b], probed)
+        assert got[b]["counts"] == (len(pk_o), nv_o, cnt), b
+        assert np.array_equal(got[b]["sorted"], srt_o), b
+        assert np.array_equal(got[b]["packets"].view(np.uint8), pk_o.view(np.uint8)), b
+        assert got[b]["fill_out"].tolist() == fo_o.tolist(), b
