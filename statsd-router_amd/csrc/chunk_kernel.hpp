@@ -184,7 +184,7 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     uint4 v[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-        v[k] = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, T0 + (uint32_t)o + 16u * k, 0, SR_TILE_LOAD_AUX));
+        v[k] = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, T0 + (uint32_t)o + 16u * k, 0, 0));
     // unconditional loads (clamped addresses): a load under a lane condition becomes a branch and a
     // wait of its own
     const uint32_t prevw = t ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, T0 - 4u, 0, 0) : 0x0A000000u;
@@ -438,11 +438,7 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
             r.offset = off;
             r.length = len > 0xFFFF ? (uint16_t)0xFFFF : (uint16_t)len;
             r.route = (uint16_t)route;
-#ifdef SR_NT_RECS
-            __builtin_nontemporal_store(*(const uint64_t *)&r, (uint64_t *)&bd.recs[rec]);
-#else
             bd.recs[rec] = r;
-#endif
             if (bd.hashes) bd.hashes[rec] = h;
         }
     };

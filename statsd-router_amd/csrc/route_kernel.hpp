@@ -68,11 +68,6 @@ constexpr uint64_t K = 65599ull;             // sdbm multiplier: (h<<6)+(h<<16)-
 constexpr int kPowLo = 64, kPowHi = 24;     // K^i (i < 64) and K^(64 i) (i < 24: exponents below 1536)
 constexpr int kPowInv = 4;                   // K^-z (z < 4)
 
-// cache policy of the tiles' 16-byte loads (developer A/B: 2 = non-temporal)
-#ifndef SR_TILE_LOAD_AUX
-#define SR_TILE_LOAD_AUX 0
-#endif
-
 // ablation switches (tools/ablate_route.hip); the product instantiates ABL_NONE
 enum : unsigned {
     ABL_NONE = 0,
@@ -1335,7 +1330,7 @@ __device__ __forceinline__ void tile_issue(const RouteParams &p, uint32_t bi, ui
     if (T0 + (uint32_t)kTileB <= bd.nbytes) {   // every tile but a batch's last: no per-piece bounds test
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-            in.v[k] = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, T0 + tid * kLaneBytes + k * 16, 0, SR_TILE_LOAD_AUX));
+            in.v[k] = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, T0 + tid * kLaneBytes + k * 16, 0, 0));
     } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) in.v[k] = load16(rsrc, T0 + tid * kLaneBytes + k * 16, bd.nbytes);
@@ -1659,11 +1654,7 @@ __device__ __forceinline__ void tile_lines(const RouteParams &p, SmemT<BLOCK> &s
                         const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
                         if (slot < p.pending_cap) p.pending[slot] = PendingLine{rec, bi, h};
                     }
-#ifdef SR_NT_RECS
-                    __builtin_nontemporal_store(*(const uint64_t *)&r, (uint64_t *)&bd.recs[rec]);
-#else
                     bd.recs[rec] = r;
-#endif
                     if (bd.hashes) bd.hashes[rec] = h;
                 }
             };

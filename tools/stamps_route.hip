@@ -47,9 +47,9 @@ void run_many(DeviceState &ds, std::vector<uint8_t *> &batches, std::vector<size
         for (int i = 0; i < L; ++i)
             DeviceState::add_batch(p, batches[i], sizes[i], d_out + (size_t)i * max_lines, max_lines, nullptr, d_n + i);
         p.dbg = d_dbg;
-        if (chunk_layout) launch_route<BLOCK, ABL_STAMPS | KV_CHUNKS>(ds, p, s);
-        else if (seg_layout) launch_route<BLOCK, ABL_STAMPS | KV_SEGMENTS>(ds, p, s);
-        else launch_route<BLOCK, ABL_STAMPS>(ds, p, s);
+        if (chunk_layout) launch_route<BLOCK, ABL_STAMPS | KV_CHUNKS | KV_ALIVE>(ds, p, s);
+        else if (seg_layout) launch_route<BLOCK, ABL_STAMPS | KV_SEGMENTS | KV_ALIVE>(ds, p, s);
+        else launch_route<BLOCK, ABL_STAMPS | KV_ALIVE>(ds, p, s);
     };
     for (int w = 0; w < 3; ++w) launch();
     CK(hipStreamSynchronize(s));
