@@ -87,9 +87,6 @@ struct sr_ctx {
 
 static void free_ptr(void *p) { (void)hipFree(p); }
 
-#ifndef SR_UNI_EXTRA
-#define SR_UNI_EXTRA 0u   // developer A/B only: extra ABL_* bits of the all-alive uniform kernel
-#endif
 #ifndef SR_CHUNK_ABL
 #define SR_CHUNK_ABL 0u   // developer ablation builds of route_chunk_kernel only (chunk_kernel.hpp)
 #endif
@@ -113,7 +110,7 @@ static int launch_product(DeviceState &ds, const RouteParams &p, hipStream_t str
     }
     if (ds.dead == 0) {   // every shard alive: the variants without the probe
         if (seg) return launch_route<kBlock, KV_SEGMENTS | KV_ALIVE>(ds, p, stream);
-        return launch_route<kBlock, KV_UNIFORM | KV_ALIVE | SR_UNI_EXTRA>(ds, p, stream);
+        return launch_route<kBlock, KV_UNIFORM | KV_ALIVE>(ds, p, stream);
     }
     if (seg) return launch_route<kBlock, KV_SEGMENTS | KV_PICKS>(ds, p, stream);
     return launch_route<kBlock, KV_UNIFORM | KV_PICKS>(ds, p, stream);
