@@ -349,3 +349,17 @@ def test_device_many_class_tables(pkg, oracle, nb, torch_stream):
             recs = d_out[i].cpu().numpy().view(pkg.RECORD_DTYPE)[:k]
             exp, _, en = oracle.route(p, 9)
             assert k == en and np.array_equal(recs, exp), f"{nb} batches: batch {i}"
+
+
+@pytest.mark.parametrize("n,dead_k", [(2, 0), (2, 1), (3, 2), (100, 99), (100, 0), (1025, 512), (65533, 65532),
+                                      (65533, 7)])
+def test_exactly_one_dead_any_size(pkg, oracle, router_factory, n, dead_k):
+    """Exactly one dead downstream (KV_DEAD1's closed-form two picks, its second reciprocal a kernel
+    argument) from N = 2 to 65533, the dead one first, last or inside: records, hashes and the
+    probed-dead bitmap (sr-main.c:106) against the restatement."""
+    alive = [1] * n
+    alive[dead_k] = 0
+    s = pkg.gen_stream(1 << 20, [64, 256, 1024], seed=n + dead_k, p_invalid=0.05)
+    r = router_factory(n, max_batch=2 << 20, alive=alive)
+    _assert_same(r.route(s.data, want_hashes=True), oracle.route(s.data, n, alive), f"N={n} dead={dead_k}")
+    assert r.last_probed_dead().tolist() == oracle.probed_dead(s.data, n, alive).tolist()
