@@ -77,6 +77,7 @@ inline RcclApi *rccl_api() {   // loaded once per process (data threads may race
 struct RebaseArgs {
     uint32_t sources;
     uint32_t n_lines;
+    uint32_t first;     // the first line that moves: sources before it land at byte 0 (source 0 always)
     uint32_t line0[kMaxOwners + 1];
     uint32_t byte0[kMaxOwners];
 };
@@ -119,6 +120,12 @@ inline int rebase_args(const sr_exchange_peer *peers, int world, RebaseArgs &a) 
     if (l > 0xFFFFFFFFull) return -EINVAL;
     a.sources = (uint32_t)world;
     a.n_lines = (uint32_t)l;
+    a.first = a.n_lines;
+    for (int q = 0; q < world; ++q)
+        if (a.byte0[q]) {
+            a.first = a.line0[q];
+            break;
+        }
     a.line0[world] = (uint32_t)l;
     return 0;
 }
@@ -166,7 +173,7 @@ inline int exchange_run(const sr_transport &t, int world, int rank, const uint64
 }
 
 __global__ __launch_bounds__(256) void exchange_rebase_kernel(sr_record *recs, RebaseArgs a) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t i = a.first + blockIdx.x * 256u + threadIdx.x;
     if (i >= a.n_lines) return;
     uint32_t lo = 0, hi = a.sources;   // the source: the last p with line0[p] <= i
     while (hi - lo > 1) {

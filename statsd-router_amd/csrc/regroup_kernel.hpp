@@ -76,37 +76,70 @@ __device__ __forceinline__ int pack_owner(const sr_record &r, uint32_t n_owners)
     return r.route < SR_ROUTE_INVALID_LENGTH ? (int)(r.route % n_owners) : -1;
 }
 
+// kCountTiles tiles per workgroup. Every load is issued before any is waited on: the {length, route}
+// words (the records' second halves) by index clamped to the batch's capacity, and the batches' line
+// counts beside them; records past the line count are masked afterwards. Gating the loads on the line
+// count serialised two memory round trips per tile.
+#ifndef SR_COUNT_TILES
+#define SR_COUNT_TILES 1
+#endif
+constexpr int kCountTiles = SR_COUNT_TILES;
+static_assert(offsetof(sr_record, length) == 4 && offsetof(sr_record, route) == 6, "{length, route} word");
 __global__ __launch_bounds__(kPackBlock) void pack_count_kernel(PackParams p) {
-    __shared__ uint32_t s_lines[kMaxOwners], s_bytes[kMaxOwners];
+    __shared__ uint32_t s_lines[kCountTiles][kMaxOwners], s_bytes[kCountTiles][kMaxOwners];
     const int tid = threadIdx.x, lane = tid & 63;
-    uint32_t r0;
-    const PackBatch &bt = pack_batch_of(p, blockIdx.x, r0);
-    const uint32_t n = (uint32_t)min(*bt.n_records, (uint64_t)bt.max_records);
     const uint32_t G = p.n_owners;
-    for (uint32_t o = tid; o < G; o += kPackBlock) s_lines[o] = s_bytes[o] = 0;
+    const uint32_t t0 = blockIdx.x * kCountTiles;
+    for (uint32_t o = tid; o < kCountTiles * G; o += kPackBlock) s_lines[o / G][o % G] = s_bytes[o / G][o % G] = 0;
+    uint32_t lr[kCountTiles][kPackChunks];
+    uint64_t nr[kCountTiles];
+    uint32_t r0s[kCountTiles], cap[kCountTiles];
+#pragma unroll
+    for (int tt = 0; tt < kCountTiles; ++tt) {
+        const uint32_t t = min(t0 + tt, p.ntiles - 1);
+        uint32_t r0;
+        const PackBatch &bt = pack_batch_of(p, t, r0);
+        r0s[tt] = r0;
+        cap[tt] = bt.max_records;
+        nr[tt] = *bt.n_records;
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(bt.recs) + 1;
+#pragma unroll
+        for (int c = 0; c < kPackChunks; ++c)
+            lr[tt][c] = w[2 * (size_t)min(r0 + c * kPackBlock + tid, bt.max_records - 1)];
+    }
     __syncthreads();
-    for (int c = 0; c < kPackChunks; ++c) {
-        const uint32_t i = r0 + c * kPackBlock + tid;
-        int ow = -1;
-        uint32_t len4 = 0;
-        if (i < n) {
-            const sr_record r = bt.recs[i];
-            ow = pack_owner(r, G);
-            len4 = pack_len4(r.length);
-        }
-        for (uint32_t o = 0; o < G; ++o) {
-            const uint64_t m = __ballot(ow == (int)o);
-            if (!m) continue;
-            const uint32_t b = wave_incl_add32(ow == (int)o ? len4 : 0u);
-            if (lane == 63) {
-                atomicAdd(&s_lines[o], (uint32_t)__popcll(m));
-                atomicAdd(&s_bytes[o], b);
+#pragma unroll
+    for (int tt = 0; tt < kCountTiles; ++tt) {
+        if (t0 + tt >= p.ntiles) break;
+        const uint32_t n = (uint32_t)min(nr[tt], (uint64_t)cap[tt]);
+#pragma unroll
+        for (int c = 0; c < kPackChunks; ++c) {
+            const uint32_t i = r0s[tt] + c * kPackBlock + tid;
+            int ow = -1;
+            uint32_t len4 = 0;
+            if (i < n) {
+                sr_record r;
+                r.length = (uint16_t)(lr[tt][c] & 0xFFFFu);
+                r.route = (uint16_t)(lr[tt][c] >> 16);
+                ow = pack_owner(r, G);
+                len4 = pack_len4(r.length);
+            }
+            for (uint32_t o = 0; o < G; ++o) {
+                const uint64_t m = __ballot(ow == (int)o);
+                if (!m) continue;
+                const uint32_t b = wave_incl_add32(ow == (int)o ? len4 : 0u);
+                if (lane == 63) {
+                    atomicAdd(&s_lines[tt][o], (uint32_t)__popcll(m));
+                    atomicAdd(&s_bytes[tt][o], b);
+                }
             }
         }
     }
     __syncthreads();
-    for (uint32_t o = tid; o < G; o += kPackBlock)
-        p.tile_counts[(size_t)blockIdx.x * G + o] = make_uint2(s_lines[o], s_bytes[o]);
+    for (uint32_t o = tid; o < kCountTiles * G; o += kPackBlock) {
+        const uint32_t tt = o / G, ow = o % G;
+        if (t0 + tt < p.ntiles) p.tile_counts[(size_t)(t0 + tt) * G + ow] = make_uint2(s_lines[tt][ow], s_bytes[tt][ow]);
+    }
 }
 
 // one workgroup: per owner, exclusive scan of the tile counts; owner totals and chunk starts
@@ -116,13 +149,22 @@ __global__ __launch_bounds__(1024) void pack_scan_kernel(PackParams p) {
     __shared__ uint32_t s_wave[16][2];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t G = p.n_owners;
+    // kScanPer consecutive tiles per thread and round: a C2 launch's 16,384 tiles in one round
+    constexpr uint32_t kScanPer = 16;
     for (uint32_t o = 0; o < G; ++o) {
         if (tid == 0) s_carry[0] = s_carry[1] = 0;
         __syncthreads();
-        for (uint32_t t0 = 0; t0 < p.ntiles; t0 += 1024) {
-            const uint32_t t = t0 + tid;
-            const uint2 v = t < p.ntiles ? p.tile_counts[(size_t)t * G + o] : make_uint2(0, 0);
-            const uint32_t il = wave_incl_add32(v.x), ib = wave_incl_add32(v.y);
+        for (uint32_t t0 = 0; t0 < p.ntiles; t0 += 1024 * kScanPer) {
+            const uint32_t tb = t0 + (uint32_t)tid * kScanPer;
+            uint2 v[kScanPer];
+            uint32_t sl = 0, sb = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kScanPer; ++k) {
+                v[k] = tb + k < p.ntiles ? p.tile_counts[(size_t)(tb + k) * G + o] : make_uint2(0, 0);
+                sl += v[k].x;
+                sb += v[k].y;
+            }
+            const uint32_t il = wave_incl_add32(sl), ib = wave_incl_add32(sb);
             if (lane == 63) {
                 s_wave[wave][0] = il;
                 s_wave[wave][1] = ib;
@@ -133,11 +175,18 @@ __global__ __launch_bounds__(1024) void pack_scan_kernel(PackParams p) {
                 pl += s_wave[w][0];
                 pb += s_wave[w][1];
             }
-            if (t < p.ntiles) p.tile_base[(size_t)t * G + o] = make_uint2(pl + il - v.x, pb + ib - v.y);
+            pl += il - sl;
+            pb += ib - sb;
+#pragma unroll
+            for (uint32_t k = 0; k < kScanPer; ++k) {
+                if (tb + k < p.ntiles) p.tile_base[(size_t)(tb + k) * G + o] = make_uint2(pl, pb);
+                pl += v[k].x;
+                pb += v[k].y;
+            }
             __syncthreads();
             if (tid == 1023) {
-                s_carry[0] = pl + il;
-                s_carry[1] = pb + ib;
+                s_carry[0] = pl;
+                s_carry[1] = pb;
             }
             __syncthreads();
         }
@@ -164,6 +213,7 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
     __shared__ uint32_t s_run_l[kMaxOwners], s_run_b[kMaxOwners];   // running in-tile position per owner
     __shared__ uint32_t s_wl[4][kMaxOwners], s_wb[4][kMaxOwners];   // per-wave chunk totals
     __shared__ uint32_t s_src[kPackBlock], s_dst[kPackBlock], s_len[kPackBlock];
+    __shared__ uint32_t s_lmax[4];   // per wave: its longest line of the chunk
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t r0;
     const PackBatch &bt = pack_batch_of(p, blockIdx.x, r0);
@@ -223,6 +273,10 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
         s_src[tid] = r.offset;
         s_dst[tid] = dst;
         s_len[tid] = ow >= 0 ? r.length | (ow == p.own ? 0x80000000u : 0u) : 0u;
+        {
+            const uint32_t lm = wave_incl_max32(ow >= 0 ? (uint32_t)r.length : 0u);
+            if (lane == 63) s_lmax[wave] = lm;
+        }
         __syncthreads();
         if (tid < (int)G) {
             uint32_t al = 0, ab = 0;
@@ -233,15 +287,18 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
             s_run_l[tid] += al;
             s_run_b[tid] += ab;
         }
-        // copy the chunk's lines: 16 lanes per line, one dword per lane per pass, 4-byte aligned
-        // destination, source realigned from two aligned dwords (buffer loads: no fault past the end)
-        // 16 lanes per line, 16 bytes per lane per pass: one dwordx4 and one dword load (the
-        // source realigned by v_alignbyte), a dwordx4 store where the padded line covers all of it;
-        // the loads of kCopyBatch passes are issued before their stores
+        // copy the chunk's lines: S lanes per line (4, 8 or 16: as few as cover the chunk's longest line
+        // in one pass, 64-byte lines four lanes), 16 bytes per lane per pass: one dwordx4 and one dword
+        // load (the source realigned by v_alignbyte), a dwordx4 store where the padded line covers all
+        // of it, 4-byte aligned destinations (buffer loads: no fault past the end); the loads of
+        // kCopyBatch passes are issued before their stores
         constexpr int kCopyBatch = 4;
-        const int sub = tid & 15;
+        const uint32_t lmax = max(max(s_lmax[0], s_lmax[1]), max(s_lmax[2], s_lmax[3]));
+        const int lg = lmax <= 64u ? 2 : (lmax <= 128u ? 3 : 4);   // block-uniform
+        const uint32_t span = 16u << lg;                           // bytes per line and pass
+        const int sub = tid & ((1 << lg) - 1);
         const uint64_t own_cap = p.own >= 0 ? p.owner_counts[2 * p.own + 1] : 0ull;
-        for (int k = tid >> 4; k < kPackBlock; k += kPackBlock / 16) {
+        for (int k = tid >> lg; k < kPackBlock; k += kPackBlock >> lg) {
             const uint32_t Lf = s_len[k];
             if (Lf == 0) continue;
             const bool mine = (Lf >> 31) != 0;
@@ -251,11 +308,11 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
             const uint32_t src = s_src[k], d = s_dst[k];
             const uint32_t sh = src & 3u, sa = src & ~3u;
             const uint32_t L4 = pack_len4(L);
-            for (uint32_t q0 = 16u * sub; q0 < L; q0 += 256u * kCopyBatch) {
+            for (uint32_t q0 = 16u * sub; q0 < L; q0 += span * kCopyBatch) {
                 uint4 v[kCopyBatch];
 #pragma unroll
                 for (int i = 0; i < kCopyBatch; ++i) {
-                    const uint32_t q = q0 + 256u * i;
+                    const uint32_t q = q0 + span * i;
                     v[i] = make_uint4(0, 0, 0, 0);
                     if (q < L) {
                         const v4u32 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, sa + q, 0, 0);
@@ -266,7 +323,7 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
                 }
 #pragma unroll
                 for (int i = 0; i < kCopyBatch; ++i) {
-                    const uint32_t q = q0 + 256u * i;
+                    const uint32_t q = q0 + span * i;
                     if (q >= L) break;
                     uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
 #pragma unroll

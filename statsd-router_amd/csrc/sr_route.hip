@@ -387,7 +387,7 @@ static int pack_launch(sr_ctx *c, const PackBatch *in, uint32_t nb, uint32_t n_o
     p.own_bytes = own_bytes;
     p.own_recs = own_recs;
     if ((phases & kPackSizes) && ntiles) {
-        hipLaunchKernelGGL(pack_count_kernel, dim3(ntiles), dim3(kPackBlock), 0, c->stream, p);
+        hipLaunchKernelGGL(pack_count_kernel, dim3((ntiles + kCountTiles - 1) / kCountTiles), dim3(kPackBlock), 0, c->stream, p);
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
     if (phases & kPackSizes) {
@@ -1101,8 +1101,8 @@ static int rebase_launch(hipStream_t stream, sr_record *d_recs, const sr_exchang
     RebaseArgs a;
     int rc = rebase_args(peers, world, a);
     if (rc) return rc;
-    if (a.n_lines) {
-        hipLaunchKernelGGL(exchange_rebase_kernel, dim3((a.n_lines + 255u) / 256u), dim3(256), 0, stream, d_recs, a);
+    if (a.n_lines > a.first) {   // (one source, or every source before the first that moves: nothing to add)
+        hipLaunchKernelGGL(exchange_rebase_kernel, dim3((a.n_lines - a.first + 255u) / 256u), dim3(256), 0, stream, d_recs, a);
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
     return 0;
