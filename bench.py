@@ -83,6 +83,8 @@ def parse(argv=None):
                     help="regroup transport: the C ABI's RCCL exchange or torch.distributed")
     ap.add_argument("--regroup-copy-own", action="store_true",
                     help="developer A/B: pack the own chunk into the packed buffer and copy it (round-4 path)")
+    ap.add_argument("--regroup-split-calls", action="store_true",
+                    help="developer A/B: the regroup's calls one by one from Python instead of sr_regroup_launch")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -382,7 +384,7 @@ def main(argv=None):
         try:   # a failing regroup leg must not take the main line with it
             rg = regroup_leg(pkg, dev, local, world, rank, args.regroup_config, args.regroup_steps,
                              per_step=args.regroup_batches, exchange=args.exchange,
-                             own_in_place=not args.regroup_copy_own)
+                             own_in_place=not args.regroup_copy_own, one_call=not args.regroup_split_calls)
         except (RuntimeError, OSError, ValueError) as e:
             rg = {"error": f"{type(e).__name__}: {e}"}
         if rank == 0:
@@ -536,7 +538,8 @@ def cpu_baseline(host, shards, alive, seconds):
     }, **common)
 
 
-def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8, exchange="c", own_in_place=True):
+def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8, exchange="c", own_in_place=True,
+                one_call=True):
     """Classify + regroup on its own batches of config `cfg` (C5 by default: mixed
     lengths, 64 shards). One step = one route launch of `per_step` batches, then ONE pack of all of
     them by owner GPU (shard % G, sr_pack_many_by_owner) and ONE exchange: an all-to-all of the
@@ -586,7 +589,8 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8, exchange="
                 comm = None
             transport += f" (sr_comm_open failed on some rank{': ' + err if err else ''})"
     with torch.cuda.stream(stream):
-        reg = rg_mod.LaunchRegrouper(pkg, router, sum(sizes), nb * max_lines, comm=comm, own_in_place=own_in_place)
+        reg = rg_mod.LaunchRegrouper(pkg, router, sum(sizes), nb * max_lines, comm=comm, own_in_place=own_in_place,
+                                      one_call=one_call)
 
         def step():
             router.route_device_many(route_descs)
@@ -620,7 +624,8 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8, exchange="
             "note": (f"route launch of {nb} x 16 MiB batches + one pack by owner + one exchange (split sizes, "
                      f"packed lines, records) per step over {world} GPU(s); owner = shard % {world}; one host round "
                      f"trip per step for the split sizes; "
-                     + ("sr_pack_owner_sizes, then sr_pack_owner_scatter with the rank's own chunk written straight "
+                     + (("sr_regroup_launch: " if one_call else "")
+                        + "sr_pack_owner_sizes, then sr_pack_owner_scatter with the rank's own chunk written straight "
                         "into the receive buffers (no local copy)" if comm is not None and own_in_place
                         else "sr_pack_many_by_owner"))}
 

@@ -222,9 +222,11 @@ void sr_comm_close(sr_comm *comm);
 
 /* Collective, on the context's stream: all-to-all of the split sizes d_owner_counts (u64
  * [world][2] {lines, bytes} per owner, the pack's output) into d_recv_counts (u64 [world][2] per
- * source rank), then one copy of both to the host: h_sent / h_received (u64 [world][2]) are valid
- * on return (the stream is synchronised: the launch's one host round trip). Returns 0, -EINVAL,
- * -EIO. */
+ * source rank; one rank: a device copy, no collective), then both to the host: h_sent / h_received
+ * (u64 [world][2]) are valid on return (the launch's one host round trip). One kernel writes them to
+ * mapped pinned memory behind a sequence word the host spins on (polling the stream for errors), so the
+ * call returns as soon as the sizes land, not when the stream drains: the caller's later work on the
+ * context's stream is ordered after them as usual. Returns 0, -EINVAL, -EIO. */
 int sr_exchange_sizes(sr_ctx *ctx, sr_comm *comm, const uint64_t *d_owner_counts, uint64_t *d_recv_counts,
                       uint64_t *h_sent, uint64_t *h_received);
 
@@ -278,6 +280,21 @@ typedef struct sr_transport {
 int sr_exchange_run(const sr_transport *t, int world, int rank, const uint64_t *h_sent,
                     const uint64_t *h_received, const uint8_t *packed, const sr_record *packed_recs,
                     uint8_t *recv_bytes, sr_record *recv_recs);
+
+/* One route launch's whole regroup in one call, for the host loop that runs it every launch:
+ * sr_pack_owner_sizes (n_owners = the comm's world), sr_exchange_sizes (the one host round trip),
+ * sr_exchange_plan, then sr_pack_owner_scatter with the rank's own chunk written into its place in the
+ * receive buffers and sr_exchange_data. Only the host work between the sizes arriving and the scatter's
+ * launch stays on the critical path (no interpreter in between). h_sent / h_received (u64 [world][2])
+ * hold the split sizes on return, also when the receive buffers are too small: then nothing is
+ * scattered or sent and -ENOSPC is returned; the caller allocates the sizes' totals (sr_exchange_plan)
+ * and finishes with sr_pack_owner_scatter and sr_exchange_data as above. packed_cap / d_packed_recs as
+ * sr_pack_many_by_owner's out_cap / d_out_recs; recv_bytes_cap / recv_recs_cap in bytes / records.
+ * Returns 0, -ENOSPC, -EINVAL, -ENOMEM, -EIO. Collective: every rank of the comm calls it. */
+int sr_regroup_launch(sr_ctx *ctx, sr_comm *comm, const sr_batch *batches, size_t count,
+                      uint64_t *d_owner_counts, uint64_t *d_recv_counts, uint8_t *d_packed, size_t packed_cap,
+                      sr_record *d_packed_recs, uint8_t *d_recv_bytes, size_t recv_bytes_cap,
+                      sr_record *d_recv_recs, size_t recv_recs_cap, uint64_t *h_sent, uint64_t *h_received);
 
 /* The rebase of sr_exchange_data alone (asynchronous on the context's stream): records
  * [peers[p].recv_line0, +recv_lines) of d_recv_recs move by peers[p].recv_byte0, p = 0..world-1.

@@ -50,7 +50,7 @@ ABI_FUNCTIONS = (
     "sr_last_layout",
     "sr_route_batch", "sr_last_probed_dead", "sr_route_device", "sr_route_device_many", "sr_pack_by_owner",
     "sr_pack_many_by_owner", "sr_pack_packets", "sr_pack_packets_many", "sr_route_pack_batch", "sr_alloc_host", "sr_free_host", "sr_sync", "sr_close", "sr_version",
-    "sr_pack_owner_sizes", "sr_pack_owner_scatter",
+    "sr_pack_owner_sizes", "sr_pack_owner_scatter", "sr_regroup_launch",
     "sr_comm_id", "sr_comm_open", "sr_comm_close", "sr_exchange_sizes", "sr_exchange_data",
     "sr_exchange_plan", "sr_exchange_run", "sr_exchange_rebase", "sr_route_pack_submit", "sr_route_pack_result",
     "sr_set_trace", "sr_route_pack_trace", "sr_set_knob", "sr_route_pack_many",
@@ -200,6 +200,8 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_exchange_run": (ctypes.c_int, [ctypes.POINTER(SrTransport), ctypes.c_int, ctypes.c_int, vp, vp, vp, vp,
                                            vp, vp]),
         "sr_exchange_rebase": (ctypes.c_int, [vp, vp, vp, ctypes.c_int]),
+        "sr_regroup_launch": (ctypes.c_int, [vp, vp, ctypes.POINTER(SrBatch), ctypes.c_size_t, vp, vp, vp,
+                                             ctypes.c_size_t, vp, vp, ctypes.c_size_t, vp, ctypes.c_size_t, vp, vp]),
         "sr_route_pack_submit": (ctypes.c_int, [vp, ctypes.c_int, vp, ctypes.c_size_t, vp]),
         "sr_route_pack_result": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(SrPackResult)]),
         "sr_set_trace": (ctypes.c_int, [vp, ctypes.c_int]),
@@ -486,11 +488,14 @@ class Router:
                                          vp(d_fill_out)), "sr_pack_packets")
 
     @staticmethod
-    def _owner_batches(batches):
+    def owner_batches(batches):
+        """The sr_batch array of [(d_bytes, nbytes, d_recs, max_records, d_n_records), ...] (reusable)."""
         arr = (SrBatch * max(len(batches), 1))()
         for i, (db, nb, dr, mr, dn) in enumerate(batches):
             arr[i] = SrBatch(db, nb, dr, mr, None, dn, None)
         return arr
+
+    _owner_batches = owner_batches
 
     def pack_many_by_owner(self, batches, n_owners: int, d_out_bytes: int, out_cap: int, d_out_recs: int,
                            d_owner_counts: int) -> None:
@@ -542,6 +547,26 @@ class Router:
         _check(self._lib.sr_exchange_sizes(self._h, comm.handle, vp(d_owner_counts), vp(d_recv_counts),
                                            sent.ctypes.data, received.ctypes.data), "sr_exchange_sizes")
         return sent, received
+
+    def regroup_launch(self, comm: "Comm", batches, d_owner_counts: int, d_recv_counts: int, d_packed: int,
+                       packed_cap: int, d_packed_recs: int, d_recv_bytes: int, recv_bytes_cap: int, d_recv_recs: int,
+                       recv_recs_cap: int):
+        """sr_regroup_launch (batches as pack_many_by_owner's, or an array from owner_batches()): returns
+        (fits, sent, received); fits False = -ENOSPC: the sizes are exchanged, nothing scattered or sent yet
+        (finish with pack_owner_scatter and exchange_data into buffers of the received totals)."""
+        sent = np.zeros((comm.world, 2), dtype=np.uint64)
+        received = np.zeros((comm.world, 2), dtype=np.uint64)
+        arr = batches if isinstance(batches, ctypes.Array) else self._owner_batches(batches)
+        n = len(batches)
+        vp = ctypes.c_void_p
+        rc = self._lib.sr_regroup_launch(self._h, comm.handle, arr, n, vp(d_owner_counts), vp(d_recv_counts),
+                                         vp(d_packed), packed_cap, vp(d_packed_recs), vp(d_recv_bytes),
+                                         recv_bytes_cap, vp(d_recv_recs), recv_recs_cap, sent.ctypes.data,
+                                         received.ctypes.data)
+        if rc == -errno.ENOSPC:
+            return False, sent, received
+        _check(rc, "sr_regroup_launch")
+        return True, sent, received
 
     def exchange_data(self, comm: "Comm", d_packed: int, d_packed_recs: int, sent: np.ndarray,
                       received: np.ndarray, d_recv_bytes: int, d_recv_recs: int) -> None:

@@ -172,6 +172,26 @@ inline int exchange_run(const sr_transport &t, int world, int rank, const uint64
     return tot[2] ? t.rebase(t.user, recv_recs, peers, world, tot[2]) : 0;
 }
 
+// The split sizes to the host in one launch (sr_exchange_sizes): sent and received {lines, bytes}
+// (u64 [world][2] each) into mapped, coherent pinned memory, then a sequence word after a system-scope
+// fence, which the host polls; no copy launches and no blocking stream synchronisation on the launch's
+// one host round trip. recv == nullptr (one rank, no collective): the received sizes are the sent ones,
+// also written to d_recv. One workgroup of 256 threads, w2 = 2 * world <= 128.
+__global__ __launch_bounds__(256) void sizes_publish_kernel(const uint64_t *sent, const uint64_t *recv,
+                                                             uint64_t *d_recv, uint64_t *h, uint32_t w2, uint64_t seq) {
+    const uint32_t t = threadIdx.x;
+    if (t < w2) {
+        const uint64_t v = sent[t];
+        h[t] = v;
+        if (!recv) d_recv[t] = v;
+    } else if (t >= 128 && t - 128 < w2) {
+        h[w2 + t - 128] = (recv ? recv : sent)[t - 128];
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) *(volatile uint64_t *)(h + 2 * w2) = seq;
+}
+
 __global__ __launch_bounds__(256) void exchange_rebase_kernel(sr_record *recs, RebaseArgs a) {
     const uint32_t i = a.first + blockIdx.x * 256u + threadIdx.x;
     if (i >= a.n_lines) return;

@@ -1035,7 +1035,9 @@ int sr_route_batch(sr_ctx *c, const uint8_t *bytes, size_t nbytes, sr_record *ou
 struct sr_comm {
     void *nccl;
     int world, rank, device;
-    uint64_t *h_sizes;   // pinned: [2][world][2] sent, received
+    uint64_t *h_sizes;   // pinned, mapped, coherent: [2][world][2] sent, received, then the sequence word
+    uint64_t *d_sizes;   // its device address (nullptr: copies and a stream synchronisation instead)
+    uint64_t seq;
 };
 
 extern "C" {
@@ -1053,12 +1055,15 @@ int sr_comm_open(sr_comm **out, const uint8_t id[SR_COMM_ID_BYTES], int world, i
     RcclApi *r = rccl_api();
     if (!r) return -ENOSYS;
     if (hipSetDevice(device) != hipSuccess) return -ENODEV;
-    sr_comm *c = new (std::nothrow) sr_comm{nullptr, world, rank, device, nullptr};
+    sr_comm *c = new (std::nothrow) sr_comm{nullptr, world, rank, device, nullptr, nullptr, 0};
     if (!c) return -ENOMEM;
-    if (hipHostMalloc((void **)&c->h_sizes, 4 * (size_t)world * sizeof(uint64_t)) != hipSuccess) {
+    if (hipHostMalloc((void **)&c->h_sizes, (4 * (size_t)world + 1) * sizeof(uint64_t),
+                      hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
         delete c;
         return -ENOMEM;
     }
+    memset(c->h_sizes, 0, (4 * (size_t)world + 1) * sizeof(uint64_t));
+    if (hipHostGetDevicePointer((void **)&c->d_sizes, c->h_sizes, 0) != hipSuccess) c->d_sizes = nullptr;
     CommId cid;
     memcpy(cid.b, id, sizeof(cid.b));
     if (((InitRankFn)r->comm_init_rank)(&c->nccl, world, cid, rank) != 0) {
@@ -1085,6 +1090,36 @@ int sr_exchange_sizes(sr_ctx *ctx, sr_comm *comm, const uint64_t *d_owner_counts
     if (!r) return -ENOSYS;
     (void)hipSetDevice(ctx->device);
     const size_t w2 = 2 * (size_t)comm->world;
+    if (comm->d_sizes) {
+        // one rank: nothing to exchange (the received sizes are the sent ones, written by the publish
+        // kernel); then the host spins on the sequence word, checking the stream now and then for errors
+        if (comm->world > 1 &&
+            r->all_to_all(d_owner_counts, d_recv_counts, 2, kNcclUint64, comm->nccl, ctx->stream) != 0)
+            return -EIO;
+        const uint64_t seq = ++comm->seq;
+        hipLaunchKernelGGL(sizes_publish_kernel, dim3(1), dim3(256), 0, ctx->stream, d_owner_counts,
+                           comm->world > 1 ? d_recv_counts : nullptr, d_recv_counts, comm->d_sizes,
+                           (uint32_t)w2, seq);
+        if (hipGetLastError() != hipSuccess) return -EIO;
+        volatile const uint64_t *hs = comm->h_sizes;
+        for (uint32_t k = 1; hs[2 * w2] != seq; ++k) {
+            if ((k & 255u) == 0) {
+                const hipError_t q = hipStreamQuery(ctx->stream);
+                if (q == hipSuccess) {
+                    if (hs[2 * w2] == seq) break;
+                    return -EIO;
+                }
+                if (q != hipErrorNotReady) return -EIO;
+            }
+            __builtin_ia32_pause();
+        }
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        for (size_t i = 0; i < w2; ++i) {
+            h_sent[i] = hs[i];
+            h_received[i] = hs[w2 + i];
+        }
+        return 0;
+    }
     if (r->all_to_all(d_owner_counts, d_recv_counts, 2, kNcclUint64, comm->nccl, ctx->stream) != 0) return -EIO;
     if (hipMemcpyAsync(comm->h_sizes, d_owner_counts, w2 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream) !=
             hipSuccess ||
@@ -1156,6 +1191,28 @@ int sr_exchange_data(sr_ctx *ctx, sr_comm *comm, const uint8_t *d_packed, const 
     ctx->own_set = 0;
     return exchange_run(t, comm->world, comm->rank, h_sent, h_received, d_packed, d_packed_recs, d_recv_bytes,
                         d_recv_recs, in_place);
+}
+
+int sr_regroup_launch(sr_ctx *ctx, sr_comm *comm, const sr_batch *batches, size_t count,
+                      uint64_t *d_owner_counts, uint64_t *d_recv_counts, uint8_t *d_packed, size_t packed_cap,
+                      sr_record *d_packed_recs, uint8_t *d_recv_bytes, size_t recv_bytes_cap,
+                      sr_record *d_recv_recs, size_t recv_recs_cap, uint64_t *h_sent, uint64_t *h_received) {
+    if (!ctx || !comm || !d_recv_bytes || !d_recv_recs || !h_sent || !h_received) return -EINVAL;
+    const uint32_t world = (uint32_t)comm->world;
+    int rc = sr_pack_owner_sizes(ctx, batches, count, world, d_owner_counts);
+    if (rc) return rc;
+    rc = sr_exchange_sizes(ctx, comm, d_owner_counts, d_recv_counts, h_sent, h_received);
+    if (rc) return rc;
+    sr_exchange_peer peers[kMaxOwners];
+    uint64_t tot[4];
+    rc = exchange_plan(comm->world, comm->rank, h_sent, h_received, peers, tot);
+    if (rc) return rc;
+    if (tot[2] > recv_recs_cap || tot[3] > recv_bytes_cap) return -ENOSPC;
+    const sr_exchange_peer &e = peers[comm->rank];
+    rc = sr_pack_owner_scatter(ctx, batches, count, world, comm->rank, d_recv_bytes + e.recv_byte0,
+                               d_recv_recs + e.recv_line0, d_packed, packed_cap, d_packed_recs);
+    if (rc) return rc;
+    return sr_exchange_data(ctx, comm, d_packed, d_packed_recs, h_sent, h_received, d_recv_bytes, d_recv_recs);
 }
 
 int sr_exchange_plan(int world, int rank, const uint64_t *h_sent, const uint64_t *h_received,

@@ -217,13 +217,16 @@ class LaunchRegrouper:
     (RCCL over xGMI with the "nccl" backend; gloo in the CPU tests). Same stream rule as Regrouper."""
 
     def __init__(self, pkg, router, max_total_bytes: int, max_total_records: int, group=None, comm=None,
-                 own_in_place: bool = True):
+                 own_in_place: bool = True, one_call: bool = True):
         """comm: a pkg.Comm for the C-ABI exchange (sr_exchange_sizes / sr_exchange_data over RCCL);
         None: torch.distributed collectives on `group` (gloo in the CPU tests, nccl on GPUs).
         own_in_place (C-ABI exchange): the pack writes the rank's own chunk straight into the receive
-        buffers; False: one sr_pack_many_by_owner and a device copy of the own chunk (A/B runs)."""
+        buffers; False: one sr_pack_many_by_owner and a device copy of the own chunk (A/B runs).
+        one_call (with own_in_place): the whole regroup in one sr_regroup_launch; False: the same work in
+        separate calls (sizes, size exchange, plan, scatter, exchange) from Python (A/B runs)."""
         self.pkg, self.router, self.group, self.comm = pkg, router, group, comm
         self.own_in_place = own_in_place
+        self.one_call = one_call
         self.G = dist.get_world_size(group)
         if not 1 <= self.G <= pkg.SR_MAX_OWNERS:
             raise ValueError(f"regroup over {self.G} ranks: at most {pkg.SR_MAX_OWNERS}")
@@ -235,6 +238,8 @@ class LaunchRegrouper:
         self.counts = torch.zeros((self.G, 2), dtype=torch.int64, device=dev)
         self.last_sent: list = []
         self.last_received: list = []
+        self.recv_cap = (max(self.cap, 4), max(max_total_records, 1))   # grown when a receive is larger
+        self._streams: dict = {}
 
     def __call__(self, batches):
         """batches = [(d_bytes, nbytes, d_recs, max_records, d_n_records), ...] routed on the router's
@@ -258,26 +263,52 @@ class LaunchRegrouper:
             return rb, rr, rc
         # the C ABI: the split sizes, one size exchange (one host round trip), then the scatter with the
         # rank's own chunk written straight into its place in the receive buffers (no local copy), the
-        # grouped sends and the rebase; receive buffers from the caching allocator's pool of the router's stream
+        # grouped sends and the rebase; receive buffers from the caching allocator's pool of the router's
+        # stream. own_in_place: all of it in one sr_regroup_launch into receive buffers allocated before the
+        # sizes are known (the largest receive so far); a receive that does not fit finishes in separate calls
+        rs = self._streams.get(h)
+        if rs is None:
+            rs = torch.cuda.ExternalStream(h, device=self.bytes.device) if h != cur else torch.cuda.current_stream()
+            self._streams[h] = rs
+        dev = self.bytes.device
         if self.own_in_place:
-            self.router.pack_owner_sizes(batches, self.G, self.counts.data_ptr())
+            with torch.cuda.stream(rs):
+                rc = torch.empty((self.G, 2), dtype=torch.int64, device=dev)
+                rb = torch.empty(self.recv_cap[0], dtype=torch.uint8, device=dev)
+                rr = torch.empty(self.recv_cap[1], dtype=torch.int64, device=dev)
+            if self.one_call:
+                fits, sent, received = self.router.regroup_launch(
+                    self.comm, batches, self.counts.data_ptr(), rc.data_ptr(), self.bytes.data_ptr(), self.cap,
+                    self.recs.data_ptr(), rb.data_ptr(), rb.numel(), rr.data_ptr(), rr.numel())
+            else:
+                self.router.pack_owner_sizes(batches, self.G, self.counts.data_ptr())
+                sent, received = self.router.exchange_sizes(self.comm, self.counts.data_ptr(), rc.data_ptr())
+                fits = False
+            n_l, n_b = int(received[:, 0].sum()), int(received[:, 1].sum())
+            if not fits:
+                if n_b > rb.numel() or n_l > rr.numel():
+                    self.recv_cap = (max(self.recv_cap[0], n_b + n_b // 4 + 4),
+                                     max(self.recv_cap[1], n_l + n_l // 4 + 1))
+                    with torch.cuda.stream(rs):
+                        rb = torch.empty(self.recv_cap[0], dtype=torch.uint8, device=dev)
+                        rr = torch.empty(self.recv_cap[1], dtype=torch.int64, device=dev)
+                peers, _ = self.pkg.exchange_plan(self.G, self.comm.rank, sent, received)
+                me = peers[self.comm.rank]
+                self.router.pack_owner_scatter(batches, self.G, self.comm.rank, rb.data_ptr() + int(me["recv_byte0"]),
+                                               rr.data_ptr() + 8 * int(me["recv_line0"]), self.bytes.data_ptr(),
+                                               self.cap, self.recs.data_ptr())
+                self.router.exchange_data(self.comm, self.bytes.data_ptr(), self.recs.data_ptr(), sent, received,
+                                          rb.data_ptr(), rr.data_ptr())
         else:
             self.router.pack_many_by_owner(batches, self.G, self.bytes.data_ptr(), self.cap, self.recs.data_ptr(),
                                            self.counts.data_ptr())
-        rs = torch.cuda.ExternalStream(h, device=self.bytes.device) if h != cur else torch.cuda.current_stream()
-        with torch.cuda.stream(rs):
-            rc = torch.empty((self.G, 2), dtype=torch.int64, device=self.bytes.device)
-            sent, received = self.router.exchange_sizes(self.comm, self.counts.data_ptr(), rc.data_ptr())
-            n_l, n_b = int(received[:, 0].sum()), int(received[:, 1].sum())
-            rb = torch.empty(max(n_b, 1), dtype=torch.uint8, device=self.bytes.device)
-            rr = torch.empty(max(n_l, 1), dtype=torch.int64, device=self.bytes.device)
-        if self.own_in_place:
-            peers, _ = self.pkg.exchange_plan(self.G, self.comm.rank, sent, received)
-            me = peers[self.comm.rank]
-            self.router.pack_owner_scatter(batches, self.G, self.comm.rank, rb.data_ptr() + int(me["recv_byte0"]),
-                                       rr.data_ptr() + 8 * int(me["recv_line0"]), self.bytes.data_ptr(), self.cap,
-                                           self.recs.data_ptr())
-        self.router.exchange_data(self.comm, self.bytes.data_ptr(), self.recs.data_ptr(), sent, received,
-                                  rb.data_ptr(), rr.data_ptr())
+            with torch.cuda.stream(rs):
+                rc = torch.empty((self.G, 2), dtype=torch.int64, device=dev)
+                sent, received = self.router.exchange_sizes(self.comm, self.counts.data_ptr(), rc.data_ptr())
+                n_l, n_b = int(received[:, 0].sum()), int(received[:, 1].sum())
+                rb = torch.empty(max(n_b, 1), dtype=torch.uint8, device=dev)
+                rr = torch.empty(max(n_l, 1), dtype=torch.int64, device=dev)
+            self.router.exchange_data(self.comm, self.bytes.data_ptr(), self.recs.data_ptr(), sent, received,
+                                      rb.data_ptr(), rr.data_ptr())
         self.last_sent, self.last_received = sent.astype(np.int64).tolist(), received.astype(np.int64).tolist()
         return rb[:n_b], rr[:n_l], rc

@@ -249,6 +249,77 @@ def test_launch_regrouper_c_exchange(pkg, oracle, torch_stream):
         dist.destroy_process_group()
 
 
+def test_regroup_launch_one_call(pkg, oracle, torch_stream):
+    """sr_regroup_launch (sizes, size exchange, own chunk scattered in place, exchange in one call) on a
+    one-rank communicator: the oracle's launch pack; receive buffers too small give -ENOSPC with the
+    sizes, and LaunchRegrouper then finishes in separate calls and grows its receive capacity."""
+    import torch
+    import torch.distributed as dist
+
+    rg = importlib.import_module("statsd-router_amd.regroup")
+    store = dist.TCPStore("127.0.0.1", 0, 1, True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1)
+    comm = None
+    try:
+        comm = pkg.Comm.from_group(0)
+        streams = [pkg.gen_stream(1 << 19, [64, 256, 1024], seed=900 + b, p_invalid=0.1) for b in range(3)]
+        cap = max(s.n_lines for s in streams)
+        d_in = torch.zeros((3, 1 << 19), dtype=torch.uint8, device="cuda")
+        for b, s in enumerate(streams):
+            d_in[b, : s.data.size].copy_(torch.from_numpy(s.data))
+        d_rec = torch.zeros((3, cap), dtype=torch.int64, device="cuda")
+        d_n = torch.zeros(3, dtype=torch.int64, device="cuda")
+        total = sum(int(s.data.size) for s in streams)
+        recs_list = [oracle.route(s.data, 16)[0] for s in streams]
+        eb, er, ec = oracle.pack_many_by_owner([s.data for s in streams], recs_list, 1)
+        with pkg.Router(16, 1 << 19) as r:
+            r.set_stream(torch_stream.cuda_stream)
+            batches = [(d_in[b].data_ptr(), int(s.data.size), d_rec[b].data_ptr(), cap, d_n[b].data_ptr())
+                       for b, s in enumerate(streams)]
+            r.route_device_many([(db, nb, dr, mr, None, dn) for db, nb, dr, mr, dn in batches])
+            pcap = pkg.pack_capacity(total)
+            packed = torch.empty(pcap, dtype=torch.uint8, device="cuda")
+            precs = torch.empty(3 * cap, dtype=torch.int64, device="cuda")
+            counts = torch.empty((1, 2), dtype=torch.int64, device="cuda")
+            rcv = torch.empty((1, 2), dtype=torch.int64, device="cuda")
+            # too small: -ENOSPC, the sizes returned, nothing written
+            rb = torch.full((16,), 0xCD, dtype=torch.uint8, device="cuda")
+            rr = torch.zeros(4, dtype=torch.int64, device="cuda")
+            fits, sent, received = r.regroup_launch(comm, batches, counts.data_ptr(), rcv.data_ptr(), packed.data_ptr(),
+                                                    pcap, precs.data_ptr(), rb.data_ptr(), rb.numel(), rr.data_ptr(),
+                                                    rr.numel())
+            torch_stream.synchronize()
+            assert not fits and received.astype(np.int64).tolist() == ec.tolist() == sent.astype(np.int64).tolist()
+            assert (rb.cpu().numpy() == 0xCD).all()
+            # large enough: the whole regroup in one call
+            n_b, n_l = int(ec[:, 1].sum()), int(ec[:, 0].sum())
+            rb = torch.full((n_b + 64,), 0xCD, dtype=torch.uint8, device="cuda")
+            rr = torch.zeros(n_l + 3, dtype=torch.int64, device="cuda")
+            fits, sent, received = r.regroup_launch(comm, r.owner_batches(batches), counts.data_ptr(), rcv.data_ptr(),
+                                                    packed.data_ptr(), pcap, precs.data_ptr(), rb.data_ptr(),
+                                                    rb.numel(), rr.data_ptr(), rr.numel())
+            torch_stream.synchronize()
+            assert fits and received.astype(np.int64).tolist() == ec.tolist()
+            got_b = rb.cpu().numpy()
+            assert np.array_equal(got_b[:n_b], eb) and (got_b[n_b:] == 0xCD).all()
+            assert np.array_equal(rr.cpu().numpy()[:n_l].view(pkg.RECORD_DTYPE), er)
+            assert rcv.cpu().numpy().tolist() == ec.tolist()
+            # LaunchRegrouper: a receive capacity below the launch's finishes in separate calls, then fits
+            reg = rg.LaunchRegrouper(pkg, r, total, 3 * cap, comm=comm)
+            reg.recv_cap = (8, 1)
+            for k in range(2):
+                rb, rr, rc = reg(batches)
+                torch_stream.synchronize()
+                assert np.array_equal(rb.cpu().numpy(), eb), k
+                assert np.array_equal(rr.cpu().numpy().view(pkg.RECORD_DTYPE), er), k
+                assert rc.cpu().numpy().tolist() == ec.tolist()
+                assert reg.recv_cap[0] >= n_b and reg.recv_cap[1] >= n_l
+    finally:
+        if comm is not None:
+            comm.close()
+        dist.destroy_process_group()
+
+
 def _three_rank_packs(pkg, oracle, world=3, n_shards=16):
     """The oracle's launch packs of `world` ranks (rank world-1 has nothing valid to send)."""
     alive = [0 if k % 7 == 3 else 1 for k in range(n_shards)]
