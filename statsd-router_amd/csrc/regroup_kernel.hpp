@@ -30,6 +30,9 @@ constexpr int kMaxOwners = 64;
 // One routed batch of a pack (up to kPackMaxBatches per pack: a route launch's batches are packed
 // and exchanged together, owner chunks holding batch 0's lines, then batch 1's, ...).
 constexpr int kPackMaxBatches = 32;
+#ifndef SR_PACK_FLAT
+#define SR_PACK_FLAT 1   // the scatter's copy as a flat list of 16-byte pieces per wave (0: lanes per line)
+#endif
 struct PackBatch {
     const uint8_t *bytes;
     const sr_record *recs;
@@ -62,9 +65,13 @@ struct PackParams {
 };
 
 // the batch of pack tile `tile` and the tile's first record in it (nb <= 32: a scan over SGPRs)
+// batch of a (wave-uniform) tile: lane j compares with batch j's first tile, one ballot (a loop over the
+// batches waited on one scalar load per batch)
 __device__ __forceinline__ const PackBatch &pack_batch_of(const PackParams &p, uint32_t tile, uint32_t &r0) {
-    uint32_t k = 0;
-    for (uint32_t j = 1; j < p.nb; ++j) k += tile >= p.b[j].tile0 ? 1u : 0u;
+    static_assert(kPackMaxBatches <= 64, "one lane per batch");
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool past = lane >= 1 && lane < p.nb && tile >= p.b[lane < kPackMaxBatches ? lane : 0].tile0;
+    const uint32_t k = (uint32_t)__popcll(__ballot(past));
     r0 = (tile - p.b[k].tile0) * kPackTile;
     return p.b[k];
 }
@@ -149,25 +156,32 @@ __global__ __launch_bounds__(1024) void pack_scan_kernel(PackParams p) {
     __shared__ uint32_t s_wave[16][2];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t G = p.n_owners;
-    // kScanPer consecutive tiles per thread and round: a C2 launch's 16,384 tiles in one round
+    // kScanPer rows of 64 consecutive tiles per wave and round (a C2 launch's 16,384 tiles in one round):
+    // coalesced loads and stores, the row scans in registers. Sixteen consecutive tiles per thread made
+    // every load touch 64 lines on the one CU (18 µs per C2 launch)
     constexpr uint32_t kScanPer = 16;
     for (uint32_t o = 0; o < G; ++o) {
         if (tid == 0) s_carry[0] = s_carry[1] = 0;
         __syncthreads();
         for (uint32_t t0 = 0; t0 < p.ntiles; t0 += 1024 * kScanPer) {
-            const uint32_t tb = t0 + (uint32_t)tid * kScanPer;
+            const uint32_t wb = t0 + (uint32_t)wave * 64 * kScanPer + lane;
             uint2 v[kScanPer];
-            uint32_t sl = 0, sb = 0;
 #pragma unroll
             for (uint32_t k = 0; k < kScanPer; ++k) {
-                v[k] = tb + k < p.ntiles ? p.tile_counts[(size_t)(tb + k) * G + o] : make_uint2(0, 0);
-                sl += v[k].x;
-                sb += v[k].y;
+                const uint32_t t = wb + k * 64;
+                v[k] = t < p.ntiles ? p.tile_counts[(size_t)t * G + o] : make_uint2(0, 0);
             }
-            const uint32_t il = wave_incl_add32(sl), ib = wave_incl_add32(sb);
-            if (lane == 63) {
-                s_wave[wave][0] = il;
-                s_wave[wave][1] = ib;
+            uint32_t rl = 0, rb = 0;   // the wave's running totals (uniform)
+#pragma unroll
+            for (uint32_t k = 0; k < kScanPer; ++k) {
+                const uint32_t il = wave_incl_add32(v[k].x), ib = wave_incl_add32(v[k].y);
+                v[k] = make_uint2(rl + il - v[k].x, rb + ib - v[k].y);   // exclusive within the wave's rows
+                rl += __builtin_amdgcn_readlane(il, 63);
+                rb += __builtin_amdgcn_readlane(ib, 63);
+            }
+            if (lane == 0) {
+                s_wave[wave][0] = rl;
+                s_wave[wave][1] = rb;
             }
             __syncthreads();
             uint32_t pl = s_carry[0], pb = s_carry[1];
@@ -175,18 +189,15 @@ __global__ __launch_bounds__(1024) void pack_scan_kernel(PackParams p) {
                 pl += s_wave[w][0];
                 pb += s_wave[w][1];
             }
-            pl += il - sl;
-            pb += ib - sb;
 #pragma unroll
             for (uint32_t k = 0; k < kScanPer; ++k) {
-                if (tb + k < p.ntiles) p.tile_base[(size_t)(tb + k) * G + o] = make_uint2(pl, pb);
-                pl += v[k].x;
-                pb += v[k].y;
+                const uint32_t t = wb + k * 64;
+                if (t < p.ntiles) p.tile_base[(size_t)t * G + o] = make_uint2(pl + v[k].x, pb + v[k].y);
             }
             __syncthreads();
             if (tid == 1023) {
-                s_carry[0] = pl;
-                s_carry[1] = pb;
+                s_carry[0] = pl + rl;
+                s_carry[1] = pb + rb;
             }
             __syncthreads();
         }
@@ -213,7 +224,11 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
     __shared__ uint32_t s_run_l[kMaxOwners], s_run_b[kMaxOwners];   // running in-tile position per owner
     __shared__ uint32_t s_wl[4][kMaxOwners], s_wb[4][kMaxOwners];   // per-wave chunk totals
     __shared__ uint32_t s_src[kPackBlock], s_dst[kPackBlock], s_len[kPackBlock];
+#if SR_PACK_FLAT
+    __shared__ uint32_t s_pre[kPackBlock];   // per wave: exclusive prefix of its lines' 16-byte pieces
+#else
     __shared__ uint32_t s_lmax[4];   // per wave: its longest line of the chunk
+#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t r0;
     const PackBatch &bt = pack_batch_of(p, blockIdx.x, r0);
@@ -273,10 +288,17 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
         s_src[tid] = r.offset;
         s_dst[tid] = dst;
         s_len[tid] = ow >= 0 ? r.length | (ow == p.own ? 0x80000000u : 0u) : 0u;
+#if SR_PACK_FLAT
+        const uint32_t npc = ow >= 0 ? ((uint32_t)r.length + 15u) >> 4 : 0u;
+        const uint32_t pinc = wave_incl_add32(npc);
+        s_pre[tid] = pinc - npc;
+        const uint32_t T = __builtin_amdgcn_readlane(pinc, 63);
+#else
         {
             const uint32_t lm = wave_incl_max32(ow >= 0 ? (uint32_t)r.length : 0u);
             if (lane == 63) s_lmax[wave] = lm;
         }
+#endif
         __syncthreads();
         if (tid < (int)G) {
             uint32_t al = 0, ab = 0;
@@ -287,17 +309,73 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
             s_run_l[tid] += al;
             s_run_b[tid] += ab;
         }
+        constexpr int kCopyBatch = 4;
+        const uint64_t own_cap = p.own >= 0 ? p.owner_counts[2 * p.own + 1] : 0ull;
+#if SR_PACK_FLAT
+        // copy the wave's 64 lines as one list of 16-byte pieces (a line of L bytes has ceil(L / 16)):
+        // lane i takes piece i, i + 64, ... and finds its line by a binary search over the wave's piece
+        // prefix, so every lane moves 16 bytes per pass whatever the mix of lengths (lanes per line left
+        // most lanes idle on mixed lines). Per piece: one dwordx4 and one dword load realigned by
+        // v_alignbyte, a dwordx4 store where the padded line covers it, zero fill after the line (buffer
+        // loads: no fault past the end); the loads of kCopyBatch passes issued before their stores
+        const uint32_t *pre = s_pre + wave * 64;
+        for (uint32_t s0 = lane; s0 < T; s0 += 64u * kCopyBatch) {
+            uint4 v[kCopyBatch];
+            uint32_t kq[kCopyBatch];   // line (6 bits) | byte within it << 6; ~0 past the end
+#pragma unroll
+            for (int i = 0; i < kCopyBatch; ++i) {
+                const uint32_t sp = s0 + 64u * i;
+                v[i] = make_uint4(0, 0, 0, 0);
+                kq[i] = ~0u;
+                if (sp < T) {
+                    uint32_t j = 0;
+#pragma unroll
+                    for (uint32_t st = 32; st; st >>= 1) j += pre[j + st] <= sp ? st : 0u;
+                    const uint32_t q = (sp - pre[j]) << 4;
+                    kq[i] = j | (q << 6);
+                    const uint32_t src = s_src[wave * 64 + j], sh = src & 3u, sa = src & ~3u;
+                    const v4u32 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, sa + q, 0, 0);
+                    const uint32_t e = __builtin_amdgcn_raw_buffer_load_b32(rsrc, sa + q + 16u, 0, 0);
+                    v[i] = make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], sh), __builtin_amdgcn_alignbyte(x[2], x[1], sh),
+                                      __builtin_amdgcn_alignbyte(x[3], x[2], sh), __builtin_amdgcn_alignbyte(e, x[3], sh));
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < kCopyBatch; ++i) {
+                if (kq[i] == ~0u) break;
+                const uint32_t k = wave * 64 + (kq[i] & 63u), q = kq[i] >> 6;
+                const uint32_t Lf = s_len[k];
+                const bool mine = (Lf >> 31) != 0;
+                const uint32_t L = Lf & 0x7FFFFFFFu, L4 = pack_len4(L), d = s_dst[k];
+                uint8_t *const out = mine ? p.own_bytes : p.out_bytes;
+                const uint64_t cap = mine ? own_cap : p.out_cap;
+                uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {   // zero fill after the line
+                    const uint32_t qj = q + 4u * jj;
+                    if (qj >= L) w[jj] = 0;
+                    else if (qj + 4u > L) w[jj] &= (1u << (8u * (L - qj))) - 1u;
+                }
+                uint8_t *o = out + d + q;
+                if (q + 16u <= L4 && (uint64_t)d + q + 16u <= cap) {
+                    *(uint4 *)o = make_uint4(w[0], w[1], w[2], w[3]);
+                } else {
+#pragma unroll
+                    for (int jj = 0; jj < 4; ++jj)
+                        if (q + 4u * jj < L4 && (uint64_t)d + q + 4u * jj + 4u <= cap) ((uint32_t *)o)[jj] = w[jj];
+                }
+            }
+        }
+#else
         // copy the chunk's lines: S lanes per line (4, 8 or 16: as few as cover the chunk's longest line
         // in one pass, 64-byte lines four lanes), 16 bytes per lane per pass: one dwordx4 and one dword
         // load (the source realigned by v_alignbyte), a dwordx4 store where the padded line covers all
         // of it, 4-byte aligned destinations (buffer loads: no fault past the end); the loads of
         // kCopyBatch passes are issued before their stores
-        constexpr int kCopyBatch = 4;
         const uint32_t lmax = max(max(s_lmax[0], s_lmax[1]), max(s_lmax[2], s_lmax[3]));
         const int lg = lmax <= 64u ? 2 : (lmax <= 128u ? 3 : 4);   // block-uniform
         const uint32_t span = 16u << lg;                           // bytes per line and pass
         const int sub = tid & ((1 << lg) - 1);
-        const uint64_t own_cap = p.own >= 0 ? p.owner_counts[2 * p.own + 1] : 0ull;
         for (int k = tid >> lg; k < kPackBlock; k += kPackBlock >> lg) {
             const uint32_t Lf = s_len[k];
             if (Lf == 0) continue;
@@ -343,6 +421,7 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
                 }
             }
         }
+#endif
         __syncthreads();
     }
 }
