@@ -196,24 +196,34 @@ __device__ __forceinline__ MtuParams mtu_view(const MtuLaunch &L, uint32_t bi) {
 // the batches b = B (mod 8): every chunk of a batch on one XCD, so that the tables, next() and packet
 // lengths the table kernel writes are read from that XCD's L2 by the emit kernel (whose chain walk
 // reads one table entry per hop). kMtuNone: past the slots.
+// (B wave-uniform, the whole wave active: lane m looks at batch x + 8m, one scan and one ballot instead
+// of a loop waiting on each batch's scalar loads in turn)
 __device__ __forceinline__ uint32_t mtu_chunk_slot(const MtuLaunch &L, uint32_t B) {
     if (!L.xcd) return B < L.chunks ? B : kMtuNone;
-    const uint32_t x = B & 7u, k = B >> 3;
-    uint32_t acc = 0;
-    for (uint32_t b = x; b < L.nb; b += 8) {
-        const uint32_t s0 = L.b[b].chunk0, s1 = b + 1 < L.nb ? L.b[b + 1].chunk0 : L.chunks;
-        if (k < acc + (s1 - s0)) return s0 + (k - acc);
-        acc += s1 - s0;
+    static_assert(kMtuMaxBatches <= 8 * 64, "one lane per batch of an XCD");
+    const uint32_t x = B & 7u, k = B >> 3, lane = threadIdx.x & 63u;
+    const uint32_t b = x + 8u * lane;
+    uint32_t s0 = 0, cnt = 0;
+    if (b < L.nb) {
+        s0 = L.b[b].chunk0;
+        cnt = (b + 1 < L.nb ? L.b[b + 1].chunk0 : L.chunks) - s0;
     }
-    return kMtuNone;
+    const uint32_t incl = wave_incl_add32(cnt);
+    const uint64_t m = __ballot(b < L.nb && k < incl);
+    if (!m) return kMtuNone;
+    const uint32_t j = (uint32_t)__ffsll((unsigned long long)m) - 1u;
+    return __builtin_amdgcn_readlane(s0, j) + (k - __builtin_amdgcn_readlane(incl - cnt, j));
 }
 
-// the batch owning global index g of a per-batch sequence starting at field `first` (nb <= 32)
+// the batch owning global index g of a per-batch sequence starting at field `first` (nb <= 32; g
+// wave-uniform, the whole wave active): lane j compares with batch j, one ballot (a loop waited on one
+// scalar load per batch)
 template <class F>
 __device__ __forceinline__ uint32_t mtu_batch_of(const MtuLaunch &L, uint32_t g, F first) {
-    uint32_t k = 0;
-    for (uint32_t j = 1; j < L.nb; ++j) k += g >= first(L.b[j]) ? 1u : 0u;
-    return k;
+    static_assert(kMtuMaxBatches <= 64, "one lane per batch");
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool past = lane >= 1 && lane < L.nb && g >= first(L.b[lane < kMtuMaxBatches ? lane : 0]);
+    return (uint32_t)__popcll(__ballot(past));
 }
 
 __device__ __forceinline__ uint32_t mtu_lines(const MtuParams &p) {
@@ -351,31 +361,36 @@ __global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuLaunch L) {
     const size_t total = (size_t)nk * ntiles;
     if (tid == 0) carry_s = 0;
     __syncthreads();
-    // 16 entries per thread and round: the route kernel's tile histograms (group mode) are 1024 tiles
-    // per 16 MiB batch, so a batch of 16 shards scans 17 k entries
+    // 16 rows of 64 consecutive entries per wave and round (coalesced loads and stores, each row scanned
+    // in registers): the route kernel's tile histograms (group mode) are 1024 tiles per 16 MiB batch, so
+    // a batch of 16 shards scans 17 k entries
     constexpr int kScanPer = 16;
     for (size_t b0 = 0; b0 < total; b0 += 1024 * kScanPer) {
+        const size_t wb = b0 + (size_t)wave * 64 * kScanPer + lane;
         uint32_t v[kScanPer], s = 0;
 #pragma unroll
         for (int k = 0; k < kScanPer; ++k) {
-            const size_t i = b0 + (size_t)tid * kScanPer + k;
+            const size_t i = wb + 64 * k;
             v[k] = i < total ? p.tile_counts[i] : 0u;
-            s += v[k];
         }
-        const uint32_t incl = wave_incl_add32(s);
-        if (lane == 63) wsum[wave] = incl;
+#pragma unroll
+        for (int k = 0; k < kScanPer; ++k) {   // v[k]: exclusive within the wave's rows; s: their total
+            const uint32_t incl = wave_incl_add32(v[k]);
+            const uint32_t x = v[k];
+            v[k] = s + incl - x;
+            s += __builtin_amdgcn_readlane(incl, 63);
+        }
+        if (lane == 0) wsum[wave] = s;
         __syncthreads();
         uint32_t before = carry_s;
         for (int w = 0; w < wave; ++w) before += wsum[w];
-        uint32_t run = before + incl - s;
 #pragma unroll
         for (int k = 0; k < kScanPer; ++k) {
-            const size_t i = b0 + (size_t)tid * kScanPer + k;
-            if (i < total) p.tile_counts[i] = run;
-            run += v[k];
+            const size_t i = wb + 64 * k;
+            if (i < total) p.tile_counts[i] = before + v[k];
         }
         __syncthreads();
-        if (tid == 1023) carry_s = run;
+        if (tid == 1023) carry_s = before + s;
         __syncthreads();
     }
     const uint32_t n = mtu_lines(p);

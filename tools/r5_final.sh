@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-5 final pass on one box, this build only: every -m gpu test; the regroup leg (own chunk in place vs copied); the default bench line and
+# Round-5 final pass on one box, this build only: every -m gpu test; the regroup leg (sr_regroup_launch, the same calls one by
+# one, own chunk copied); the default bench line and
 # C2..C5 lines (all alive and 25 % dead) with route + pack; rocprofv3 kernel stats of the default
 # command for C2 and C5; the PMC traffic of the default command (copied to ./bench_traffic.json
 # afterwards: it names the library it was measured with); C1 over loopback with 10 s blasts against round 2's data thread and the
@@ -55,9 +56,9 @@ PY
   pmc)
     bash tools/r4_pmc.sh $T c2 || exit 1 ;;   # gpurun_out/${T}_bench_traffic_c2.json -> ./bench_traffic.json here
   regroup)
-    for c in c5 c2; do
-      for mode in inplace copy; do
-        extra=""; [ $mode = copy ] && extra="--regroup-copy-own"
+    for c in c5 c2 c3; do
+      for mode in inplace split copy; do
+        extra=""; [ $mode = copy ] && extra="--regroup-copy-own"; [ $mode = split ] && extra="--regroup-split-calls"
         timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu --no-e2e --no-pack --regroup on --regroup-config $c \
           --regroup-steps 32 $extra > gpurun_out/${T}_regroup_${c}_$mode.json 2> gpurun_out/${T}_regroup_${c}_$mode.err \
           || { tail -20 gpurun_out/${T}_regroup_${c}_$mode.err; exit 1; }
