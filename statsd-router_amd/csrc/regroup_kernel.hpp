@@ -30,6 +30,12 @@ constexpr int kMaxOwners = 64;
 // One routed batch of a pack (up to kPackMaxBatches per pack: a route launch's batches are packed
 // and exchanged together, owner chunks holding batch 0's lines, then batch 1's, ...).
 constexpr int kPackMaxBatches = 32;
+#ifndef SR_PACK_UNALIGNED
+#define SR_PACK_UNALIGNED 1   // the copy's 16-byte loads at the line's byte offset (0: dword-aligned loads
+#endif                        // realigned by v_alignbyte, one more load and four VALU per piece)
+#ifndef SR_PACK_COPY_BATCH
+#define SR_PACK_COPY_BATCH 4   // the owner scatter's copy passes whose loads are issued together
+#endif
 #ifndef SR_PACK_FLAT
 #define SR_PACK_FLAT 1   // the scatter's copy as a flat list of 16-byte pieces per wave (0: lanes per line)
 #endif
@@ -309,15 +315,16 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
             s_run_l[tid] += al;
             s_run_b[tid] += ab;
         }
-        constexpr int kCopyBatch = 4;
+        constexpr int kCopyBatch = SR_PACK_COPY_BATCH;
         const uint64_t own_cap = p.own >= 0 ? p.owner_counts[2 * p.own + 1] : 0ull;
 #if SR_PACK_FLAT
         // copy the wave's 64 lines as one list of 16-byte pieces (a line of L bytes has ceil(L / 16)):
         // lane i takes piece i, i + 64, ... and finds its line by a binary search over the wave's piece
         // prefix, so every lane moves 16 bytes per pass whatever the mix of lengths (lanes per line left
-        // most lanes idle on mixed lines). Per piece: one dwordx4 and one dword load realigned by
-        // v_alignbyte, a dwordx4 store where the padded line covers it, zero fill after the line (buffer
-        // loads: no fault past the end); the loads of kCopyBatch passes issued before their stores
+        // most lanes idle on mixed lines). Per piece: one dwordx4 buffer load at the source's byte offset
+        // (unaligned buffer access), a dwordx4 store where the padded line covers it, zero fill after the
+        // line (buffer loads: no fault past the end); the loads of kCopyBatch passes issued before their
+        // stores
         const uint32_t *pre = s_pre + wave * 64;
         for (uint32_t s0 = lane; s0 < T; s0 += 64u * kCopyBatch) {
             uint4 v[kCopyBatch];
@@ -333,11 +340,17 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
                     for (uint32_t st = 32; st; st >>= 1) j += pre[j + st] <= sp ? st : 0u;
                     const uint32_t q = (sp - pre[j]) << 4;
                     kq[i] = j | (q << 6);
-                    const uint32_t src = s_src[wave * 64 + j], sh = src & 3u, sa = src & ~3u;
+                    const uint32_t src = s_src[wave * 64 + j];
+#if SR_PACK_UNALIGNED
+                    const v4u32 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, src + q, 0, 0);
+                    v[i] = make_uint4(x[0], x[1], x[2], x[3]);
+#else
+                    const uint32_t sh = src & 3u, sa = src & ~3u;
                     const v4u32 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, sa + q, 0, 0);
                     const uint32_t e = __builtin_amdgcn_raw_buffer_load_b32(rsrc, sa + q + 16u, 0, 0);
                     v[i] = make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], sh), __builtin_amdgcn_alignbyte(x[2], x[1], sh),
                                       __builtin_amdgcn_alignbyte(x[3], x[2], sh), __builtin_amdgcn_alignbyte(e, x[3], sh));
+#endif
                 }
             }
 #pragma unroll
