@@ -22,7 +22,10 @@
 namespace srk {
 
 constexpr int kPackBlock = 256;
-constexpr int kPackChunks = 2;                          // 256-record chunks per tile (long lines:
+#ifndef SR_PACK_CHUNKS
+#define SR_PACK_CHUNKS 2
+#endif
+constexpr int kPackChunks = SR_PACK_CHUNKS;                          // 256-record chunks per tile (long lines:
                                                         // enough tiles to fill the chip)
 constexpr int kPackTile = kPackBlock * kPackChunks;     // records per tile
 constexpr int kMaxOwners = 64;
