@@ -197,8 +197,12 @@ int sr_pack_many_by_owner(sr_ctx *ctx, const sr_batch *batches, size_t count, ui
  *   the chunk as always), every other owner's to d_out_bytes / d_out_recs at the usual places (out_cap as
  *   sr_pack_many_by_owner). With own = the comm's rank and d_own_* = d_recv_bytes + recv_byte0 /
  *   d_recv_recs + recv_line0 of peers[rank] (sr_exchange_plan), the following sr_exchange_data on this
- *   context skips the own chunk's copies. d_own_bytes must be 4-byte aligned. Both asynchronous on the
- *   context's stream. Returns 0, -EINVAL (scatter without sizes, own out of range), -ENOMEM, -EIO. */
+ *   context skips the own chunk's copies. d_own_bytes must be 4-byte aligned. own = -1: every chunk to
+ *   d_out_bytes / d_out_recs (sr_pack_many_by_owner's output; d_own_* unused). Both asynchronous on the
+ *   context's stream. Returns 0, -EINVAL (scatter without sizes, own out of range), -ENOMEM, -EIO.
+ * The two calls pair one to one: the scatter uses the tile bases and split sizes of the context's last
+ * sizes call, and must be given the same batch descriptors and n_owners (else -EINVAL); a sizes call in
+ * between replaces them. */
 int sr_pack_owner_sizes(sr_ctx *ctx, const sr_batch *batches, size_t count, uint32_t n_owners,
                         uint64_t *d_owner_counts);
 int sr_pack_owner_scatter(sr_ctx *ctx, const sr_batch *batches, size_t count, uint32_t n_owners, int own,
@@ -295,6 +299,24 @@ int sr_regroup_launch(sr_ctx *ctx, sr_comm *comm, const sr_batch *batches, size_
                       uint64_t *d_owner_counts, uint64_t *d_recv_counts, uint8_t *d_packed, size_t packed_cap,
                       sr_record *d_packed_recs, uint8_t *d_recv_bytes, size_t recv_bytes_cap,
                       sr_record *d_recv_recs, size_t recv_recs_cap, uint64_t *h_sent, uint64_t *h_received);
+
+/* sr_regroup_launch on any transport: the same sequence (split sizes, size exchange, plan, scatter with
+ * the own chunk in place, exchange without the own chunk's copy, rebase) with `sizes` in place of
+ * sr_exchange_sizes and `t` in place of RCCL; sr_regroup_launch is this call on RCCL. `sizes` gets t->user
+ * and must leave h_sent / h_received (u64 [world][2]) valid and d_recv_counts written (ordered before
+ * the context's later work) when it returns; it is collective like the transport. The device work of the
+ * call is enqueued on the context's stream and not waited for: a transport that reads or writes device
+ * buffers from the host first waits for that stream (sr_sync). Used to run the multi-rank sequence
+ * without RCCL (ranks as threads on one GPU, or processes over gloo). Returns as sr_regroup_launch; after
+ * -ENOSPC (the sizes exchanged, nothing scattered or sent: the peers' sends to this rank stay posted)
+ * the caller finishes with sr_pack_owner_scatter (own = -1) and sr_exchange_run on the same transport. */
+typedef int (*sr_sizes_fn)(void *user, const uint64_t *d_owner_counts, uint64_t *d_recv_counts, uint64_t *h_sent,
+                           uint64_t *h_received);
+int sr_regroup_run(sr_ctx *ctx, const sr_transport *t, sr_sizes_fn sizes, int world, int rank,
+                   const sr_batch *batches, size_t count, uint64_t *d_owner_counts, uint64_t *d_recv_counts,
+                   uint8_t *d_packed, size_t packed_cap, sr_record *d_packed_recs, uint8_t *d_recv_bytes,
+                   size_t recv_bytes_cap, sr_record *d_recv_recs, size_t recv_recs_cap, uint64_t *h_sent,
+                   uint64_t *h_received);
 
 /* The rebase of sr_exchange_data alone (asynchronous on the context's stream): records
  * [peers[p].recv_line0, +recv_lines) of d_recv_recs move by peers[p].recv_byte0, p = 0..world-1.
@@ -423,9 +445,6 @@ int sr_route_pack_trace(sr_ctx *ctx, int slot, const sr_record **records, const 
  *   SR_KNOB_MTU_CHUNK     packing chunk lines: 0 = by the launch's shape (default), 2048 or 4608;
  *   SR_KNOB_MTU_XCD       1 (default): batches' packing chunks on one XCD from eight batches up;
  *   SR_KNOB_MTU_WALK      1 (default): the chain walked inside mtu_emit up to 64 shards; 0: mtu_chain;
- *   SR_KNOB_PERSIST       launches with every shard alive run the persistent chunk kernel: 0 never,
- *                         1 in the chunk layout, 2 in every layout (developer builds only, measured
- *                         slower: -ENOTSUP otherwise);
  *   SR_KNOB_HIST          1 (default): sr_route_pack_many / sr_route_pack_* hand the route kernel's tile
  *                         histograms to the packing; 0: the packing counts the records itself;
  *   SR_KNOB_PREFETCH      tiles ahead (default 96; 0 off; up to 4096) whose 128-byte lines a chunk-layout
@@ -434,13 +453,12 @@ int sr_route_pack_trace(sr_ctx *ctx, int slot, const sr_record **records, const 
  *   SR_KNOB_FUSE_DEFER    1: a route + pack launch with two or more (at most 16) dead shards leaves its
  *                         deferred probes to the packing's counting pass; 0 (default): probe_defer_kernel
  *                         (measured level on C3 / C5, slower on C4).
- * Returns 0, -EINVAL (unknown knob or value) or -ENOTSUP. */
+ * Returns 0 or -EINVAL (unknown knob or value). */
 #define SR_KNOB_LB_SPIN 1
 #define SR_KNOB_DEFER_PICKS 2
 #define SR_KNOB_MTU_CHUNK 3
 #define SR_KNOB_MTU_XCD 4
 #define SR_KNOB_MTU_WALK 5
-#define SR_KNOB_PERSIST 6
 #define SR_KNOB_HIST 7
 #define SR_KNOB_PREFETCH 8
 #define SR_KNOB_FUSE_DEFER 9

@@ -53,13 +53,13 @@ ABI_FUNCTIONS = (
     "sr_pack_owner_sizes", "sr_pack_owner_scatter", "sr_regroup_launch",
     "sr_comm_id", "sr_comm_open", "sr_comm_close", "sr_exchange_sizes", "sr_exchange_data",
     "sr_exchange_plan", "sr_exchange_run", "sr_exchange_rebase", "sr_route_pack_submit", "sr_route_pack_result",
-    "sr_set_trace", "sr_route_pack_trace", "sr_set_knob", "sr_route_pack_many",
+    "sr_set_trace", "sr_route_pack_trace", "sr_set_knob", "sr_route_pack_many", "sr_regroup_run",
 )
 SR_MAX_PACK_DOWNSTREAMS = 4096
 SR_LAYOUT_AUTO, SR_LAYOUT_UNIFORM, SR_LAYOUT_SEGMENTS, SR_LAYOUT_CHUNKS = 0, 1, 2, 3
 SR_COMM_ID_BYTES = 128
 # sr_set_knob (developer / test knobs of one context; none changes a result)
-SR_KNOB_LB_SPIN, SR_KNOB_DEFER_PICKS, SR_KNOB_MTU_CHUNK, SR_KNOB_MTU_XCD, SR_KNOB_MTU_WALK, SR_KNOB_PERSIST = 1, 2, 3, 4, 5, 6
+SR_KNOB_LB_SPIN, SR_KNOB_DEFER_PICKS, SR_KNOB_MTU_CHUNK, SR_KNOB_MTU_XCD, SR_KNOB_MTU_WALK = 1, 2, 3, 4, 5
 SR_KNOB_HIST, SR_KNOB_PREFETCH, SR_KNOB_FUSE_DEFER = 7, 8, 9
 LAYOUT_NAMES = {0: "none", 1: "uniform", 2: "segments", 3: "chunks"}
 PACKET_DTYPE = np.dtype([("first", "<u4"), ("nlines", "<u2"), ("shard", "<u2"), ("length", "<u2"),
@@ -119,6 +119,8 @@ _SEND_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctyp
 _COPY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 _REBASE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(SrExchangePeer),
                               ctypes.c_int, ctypes.c_uint64)
+_SIZES_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_void_p)
 
 
 class SrTransport(ctypes.Structure):
@@ -208,6 +210,9 @@ def _load_route_lib() -> ctypes.CDLL:
         "sr_route_pack_trace": (ctypes.c_int, [vp, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), c_size_p]),
         "sr_set_knob": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int64]),
         "sr_route_pack_many": (ctypes.c_int, [vp, ctypes.POINTER(SrBatch), ctypes.POINTER(SrPackBatch), ctypes.c_size_t]),
+        "sr_regroup_run": (ctypes.c_int, [vp, ctypes.POINTER(SrTransport), _SIZES_FN, ctypes.c_int, ctypes.c_int,
+                                          ctypes.POINTER(SrBatch), ctypes.c_size_t, vp, vp, vp, ctypes.c_size_t, vp, vp,
+                                          ctypes.c_size_t, vp, ctypes.c_size_t, vp, vp]),
     }
     for name in ABI_FUNCTIONS:
         if os.environ.get("SR_ROUTE_LIB") and not hasattr(lib, name):
@@ -568,6 +573,43 @@ class Router:
         _check(rc, "sr_regroup_launch")
         return True, sent, received
 
+    def regroup_run(self, transport: "Transport", world: int, rank: int, batches, d_owner_counts: int,
+                    d_recv_counts: int, d_packed: int, packed_cap: int, d_packed_recs: int, d_recv_bytes: int,
+                    recv_bytes_cap: int, d_recv_recs: int, recv_recs_cap: int):
+        """sr_regroup_run: regroup_launch's sequence on a Python transport whose sizes(d_owner_counts,
+        d_recv_counts) does the size exchange (returns (sent, received) [world, 2] and writes d_recv_counts).
+        Returns (fits, sent, received) as regroup_launch."""
+        sent = np.zeros((world, 2), dtype=np.uint64)
+        received = np.zeros((world, 2), dtype=np.uint64)
+        err = []
+        cb = _transport_struct(transport, err)
+
+        def sizes(_u, d_cnt, d_rcv, h_s, h_r):
+            try:
+                s_, r_ = transport.sizes(int(d_cnt or 0), int(d_rcv or 0))
+                hs = np.frombuffer((ctypes.c_uint8 * (16 * world)).from_address(h_s), dtype=np.uint64)
+                hr = np.frombuffer((ctypes.c_uint8 * (16 * world)).from_address(h_r), dtype=np.uint64)
+                hs[:] = np.asarray(s_, dtype=np.uint64).reshape(-1)
+                hr[:] = np.asarray(r_, dtype=np.uint64).reshape(-1)
+                return 0
+            except Exception as e:   # noqa: BLE001 - reported after the C call returns
+                err.append(e)
+                return -errno.EIO
+
+        sizes_fn = _SIZES_FN(sizes)
+        arr = batches if isinstance(batches, ctypes.Array) else self._owner_batches(batches)
+        vp = ctypes.c_void_p
+        rc = self._lib.sr_regroup_run(self._h, ctypes.byref(cb), sizes_fn, world, rank, arr, len(batches),
+                                      vp(d_owner_counts), vp(d_recv_counts), vp(d_packed), packed_cap,
+                                      vp(d_packed_recs), vp(d_recv_bytes), recv_bytes_cap, vp(d_recv_recs),
+                                      recv_recs_cap, sent.ctypes.data, received.ctypes.data)
+        if err:
+            raise err[0]
+        if rc == -errno.ENOSPC:
+            return False, sent, received
+        _check(rc, "sr_regroup_run")
+        return True, sent, received
+
     def exchange_data(self, comm: "Comm", d_packed: int, d_packed_recs: int, sent: np.ndarray,
                       received: np.ndarray, d_recv_bytes: int, d_recv_recs: int) -> None:
         """sr_exchange_data (asynchronous on the router's stream)."""
@@ -660,6 +702,11 @@ class Transport:
     def copy(self, dst: int, src: int, nbytes: int) -> None:
         ctypes.memmove(dst, src, nbytes)
 
+    def sizes(self, d_owner_counts: int, d_recv_counts: int):
+        """sr_regroup_run's size exchange: returns (sent, received) u64 [world, 2] and writes the received
+        sizes to d_recv_counts."""
+        raise NotImplementedError
+
     def rebase(self, recs_addr: int, peers: np.ndarray, n_lines: int) -> None:
         """Host memory: records [recv_line0, +recv_lines) of every source move by its recv_byte0."""
         recs = host_records(recs_addr, n_lines)
@@ -675,11 +722,9 @@ def host_records(addr: int, n: int) -> np.ndarray:
     return np.frombuffer((ctypes.c_uint8 * (8 * n)).from_address(addr), dtype=RECORD_DTYPE)
 
 
-def exchange_run(transport: Transport, world: int, rank: int, sent, received, packed: int, packed_recs: int,
-                 recv_bytes: int, recv_recs: int) -> None:
-    """sr_exchange_run: the C exchange plan and its calls, on a Python transport."""
-    err = []
-
+def _transport_struct(transport: Transport, err: list) -> SrTransport:
+    """An SrTransport whose callbacks call the Python transport; exceptions go to err (the callback
+    returns -EIO). Keep the returned structure alive for the duration of the C call."""
     def wrap(fn):
         def call(*a):
             try:
@@ -694,13 +739,20 @@ def exchange_run(transport: Transport, world: int, rank: int, sent, received, pa
         arr = np.ctypeslib.as_array(ctypes.cast(peers_p, ctypes.POINTER(ctypes.c_uint64)), shape=(w * 8,))
         transport.rebase(recs, arr.copy().view(PEER_DTYPE), int(n))
 
-    cb = SrTransport(None,
-                     _GROUP_FN(wrap(lambda _u: transport.group_start())),
-                     _GROUP_FN(wrap(lambda _u: transport.group_end())),
-                     _SEND_FN(wrap(lambda _u, b, n, p, t: transport.send(b, n, p, t))),
-                     _SEND_FN(wrap(lambda _u, b, n, p, t: transport.recv(b, n, p, t))),
-                     _COPY_FN(wrap(lambda _u, d, s, n: transport.copy(d, s, n))),
-                     _REBASE_FN(wrap(rebase)))
+    return SrTransport(None,
+                       _GROUP_FN(wrap(lambda _u: transport.group_start())),
+                       _GROUP_FN(wrap(lambda _u: transport.group_end())),
+                       _SEND_FN(wrap(lambda _u, b, n, p, t: transport.send(b, n, p, t))),
+                       _SEND_FN(wrap(lambda _u, b, n, p, t: transport.recv(b, n, p, t))),
+                       _COPY_FN(wrap(lambda _u, d, s, n: transport.copy(d, s, n))),
+                       _REBASE_FN(wrap(rebase)))
+
+
+def exchange_run(transport: Transport, world: int, rank: int, sent, received, packed: int, packed_recs: int,
+                 recv_bytes: int, recv_recs: int) -> None:
+    """sr_exchange_run: the C exchange plan and its calls, on a Python transport."""
+    err = []
+    cb = _transport_struct(transport, err)
     s = np.ascontiguousarray(sent, dtype=np.uint64).reshape(-1)
     r = np.ascontiguousarray(received, dtype=np.uint64).reshape(-1)
     if s.size != 2 * world or r.size != 2 * world:

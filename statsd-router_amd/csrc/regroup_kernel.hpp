@@ -33,14 +33,8 @@ constexpr int kMaxOwners = 64;
 // One routed batch of a pack (up to kPackMaxBatches per pack: a route launch's batches are packed
 // and exchanged together, owner chunks holding batch 0's lines, then batch 1's, ...).
 constexpr int kPackMaxBatches = 32;
-#ifndef SR_PACK_UNALIGNED
-#define SR_PACK_UNALIGNED 1   // the copy's 16-byte loads at the line's byte offset (0: dword-aligned loads
-#endif                        // realigned by v_alignbyte, one more load and four VALU per piece)
 #ifndef SR_PACK_COPY_BATCH
 #define SR_PACK_COPY_BATCH 4   // the owner scatter's copy passes whose loads are issued together
-#endif
-#ifndef SR_PACK_FLAT
-#define SR_PACK_FLAT 1   // the scatter's copy as a flat list of 16-byte pieces per wave (0: lanes per line)
 #endif
 struct PackBatch {
     const uint8_t *bytes;
@@ -233,11 +227,7 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
     __shared__ uint32_t s_run_l[kMaxOwners], s_run_b[kMaxOwners];   // running in-tile position per owner
     __shared__ uint32_t s_wl[4][kMaxOwners], s_wb[4][kMaxOwners];   // per-wave chunk totals
     __shared__ uint32_t s_src[kPackBlock], s_dst[kPackBlock], s_len[kPackBlock];
-#if SR_PACK_FLAT
     __shared__ uint32_t s_pre[kPackBlock];   // per wave: exclusive prefix of its lines' 16-byte pieces
-#else
-    __shared__ uint32_t s_lmax[4];   // per wave: its longest line of the chunk
-#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t r0;
     const PackBatch &bt = pack_batch_of(p, blockIdx.x, r0);
@@ -297,17 +287,10 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
         s_src[tid] = r.offset;
         s_dst[tid] = dst;
         s_len[tid] = ow >= 0 ? r.length | (ow == p.own ? 0x80000000u : 0u) : 0u;
-#if SR_PACK_FLAT
         const uint32_t npc = ow >= 0 ? ((uint32_t)r.length + 15u) >> 4 : 0u;
         const uint32_t pinc = wave_incl_add32(npc);
         s_pre[tid] = pinc - npc;
         const uint32_t T = __builtin_amdgcn_readlane(pinc, 63);
-#else
-        {
-            const uint32_t lm = wave_incl_max32(ow >= 0 ? (uint32_t)r.length : 0u);
-            if (lane == 63) s_lmax[wave] = lm;
-        }
-#endif
         __syncthreads();
         if (tid < (int)G) {
             uint32_t al = 0, ab = 0;
@@ -320,14 +303,13 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
         }
         constexpr int kCopyBatch = SR_PACK_COPY_BATCH;
         const uint64_t own_cap = p.own >= 0 ? p.owner_counts[2 * p.own + 1] : 0ull;
-#if SR_PACK_FLAT
         // copy the wave's 64 lines as one list of 16-byte pieces (a line of L bytes has ceil(L / 16)):
         // lane i takes piece i, i + 64, ... and finds its line by a binary search over the wave's piece
         // prefix, so every lane moves 16 bytes per pass whatever the mix of lengths (lanes per line left
         // most lanes idle on mixed lines). Per piece: one dwordx4 buffer load at the source's byte offset
-        // (unaligned buffer access), a dwordx4 store where the padded line covers it, zero fill after the
-        // line (buffer loads: no fault past the end); the loads of kCopyBatch passes issued before their
-        // stores
+        // (unaligned buffer access; byte loads for the one piece that crosses the batch's end), a dwordx4
+        // store where the padded line covers it, zero fill after the line; the loads of kCopyBatch passes
+        // issued before their stores
         const uint32_t *pre = s_pre + wave * 64;
         for (uint32_t s0 = lane; s0 < T; s0 += 64u * kCopyBatch) {
             uint4 v[kCopyBatch];
@@ -343,17 +325,9 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
                     for (uint32_t st = 32; st; st >>= 1) j += pre[j + st] <= sp ? st : 0u;
                     const uint32_t q = (sp - pre[j]) << 4;
                     kq[i] = j | (q << 6);
-                    const uint32_t src = s_src[wave * 64 + j];
-#if SR_PACK_UNALIGNED
-                    const v4u32 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, src + q, 0, 0);
-                    v[i] = make_uint4(x[0], x[1], x[2], x[3]);
-#else
-                    const uint32_t sh = src & 3u, sa = src & ~3u;
-                    const v4u32 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, sa + q, 0, 0);
-                    const uint32_t e = __builtin_amdgcn_raw_buffer_load_b32(rsrc, sa + q + 16u, 0, 0);
-                    v[i] = make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], sh), __builtin_amdgcn_alignbyte(x[2], x[1], sh),
-                                      __builtin_amdgcn_alignbyte(x[3], x[2], sh), __builtin_amdgcn_alignbyte(e, x[3], sh));
-#endif
+                    // the piece that straddles the batch's end by bytes (a 16-byte buffer load's range
+                    // check is not byte-exact: bytes before the end could read as zero)
+                    v[i] = load16(rsrc, s_src[wave * 64 + j] + q, bt.nbytes);
                 }
             }
 #pragma unroll
@@ -382,62 +356,6 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
                 }
             }
         }
-#else
-        // copy the chunk's lines: S lanes per line (4, 8 or 16: as few as cover the chunk's longest line
-        // in one pass, 64-byte lines four lanes), 16 bytes per lane per pass: one dwordx4 and one dword
-        // load (the source realigned by v_alignbyte), a dwordx4 store where the padded line covers all
-        // of it, 4-byte aligned destinations (buffer loads: no fault past the end); the loads of
-        // kCopyBatch passes are issued before their stores
-        const uint32_t lmax = max(max(s_lmax[0], s_lmax[1]), max(s_lmax[2], s_lmax[3]));
-        const int lg = lmax <= 64u ? 2 : (lmax <= 128u ? 3 : 4);   // block-uniform
-        const uint32_t span = 16u << lg;                           // bytes per line and pass
-        const int sub = tid & ((1 << lg) - 1);
-        for (int k = tid >> lg; k < kPackBlock; k += kPackBlock >> lg) {
-            const uint32_t Lf = s_len[k];
-            if (Lf == 0) continue;
-            const bool mine = (Lf >> 31) != 0;
-            const uint32_t L = Lf & 0x7FFFFFFFu;
-            uint8_t *const out = mine ? p.own_bytes : p.out_bytes;
-            const uint64_t cap = mine ? own_cap : p.out_cap;
-            const uint32_t src = s_src[k], d = s_dst[k];
-            const uint32_t sh = src & 3u, sa = src & ~3u;
-            const uint32_t L4 = pack_len4(L);
-            for (uint32_t q0 = 16u * sub; q0 < L; q0 += span * kCopyBatch) {
-                uint4 v[kCopyBatch];
-#pragma unroll
-                for (int i = 0; i < kCopyBatch; ++i) {
-                    const uint32_t q = q0 + span * i;
-                    v[i] = make_uint4(0, 0, 0, 0);
-                    if (q < L) {
-                        const v4u32 x = __builtin_amdgcn_raw_buffer_load_b128(rsrc, sa + q, 0, 0);
-                        const uint32_t e = __builtin_amdgcn_raw_buffer_load_b32(rsrc, sa + q + 16u, 0, 0);
-                        v[i] = make_uint4(__builtin_amdgcn_alignbyte(x[1], x[0], sh), __builtin_amdgcn_alignbyte(x[2], x[1], sh),
-                                          __builtin_amdgcn_alignbyte(x[3], x[2], sh), __builtin_amdgcn_alignbyte(e, x[3], sh));
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < kCopyBatch; ++i) {
-                    const uint32_t q = q0 + span * i;
-                    if (q >= L) break;
-                    uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {   // zero fill after the line
-                        const uint32_t qj = q + 4u * j;
-                        if (qj >= L) w[j] = 0;
-                        else if (qj + 4u > L) w[j] &= (1u << (8u * (L - qj))) - 1u;
-                    }
-                    uint8_t *o = out + d + q;
-                    if (q + 16u <= L4 && (uint64_t)d + q + 16u <= cap) {
-                        *(uint4 *)o = make_uint4(w[0], w[1], w[2], w[3]);
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            if (q + 4u * j < L4 && (uint64_t)d + q + 4u * j + 4u <= cap) ((uint32_t *)o)[j] = w[j];
-                    }
-                }
-            }
-        }
-#endif
         __syncthreads();
     }
 }

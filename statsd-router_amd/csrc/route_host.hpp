@@ -13,9 +13,6 @@
 #include <vector>
 
 #include "chunk_kernel.hpp"
-#ifdef SR_PERSIST_KERNEL   // developer builds only (`make VARIANTS=1`): measured slower, DESIGN.md §9
-#include "persist_kernel.hpp"
-#endif
 
 namespace srk {
 
@@ -101,9 +98,6 @@ struct DeviceState {
     // than 2; with one dead shard nothing is deferred at 2 picks, and deferring a quarter of the
     // lines cost C2 +30 %); SR_KNOB_DEFER_PICKS = 2 overrides (sr_set_knob)
     uint32_t defer_picks = 1;
-    // SR_KNOB_PERSIST: all-alive launches in the chunk layout (1), or in any layout (2), run the
-    // persistent kernel (route_persist_kernel); 0: never
-    uint32_t persist = 0;
     uint32_t *d_hist = nullptr;      // RouteParams::hist (sr_route_pack_many), max_tiles x kHistKeys
     bool last_hist = false;          // the last launch wrote its tiles' key histograms
     // fused deferral (route + pack launches, SR_KNOB_FUSE_DEFER, off by default): asked for by the caller, and whether
@@ -111,7 +105,6 @@ struct DeviceState {
     bool fuse_defer = false, last_fused = false;
     uint32_t fd_mark = 0;
     const uint64_t *fd_dhash[kMaxBatches] = {};
-    uint32_t persist_slots = 0;      // resident route_persist_kernel workgroups on the device (0: not yet asked)
 
     int init(size_t max_batch_bytes, uint32_t n_downstreams) {
         max_batch = max_batch_bytes;
@@ -467,33 +460,6 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
     // probe_defer_kernel, which notes the dead shards it visits; the route kernel need not
     p.mark_tiles = (p.mark && !(p.defer && p.picks == 1)) ? 1u : 0u;
     if (ds.wide() && hipMemsetAsync(&ds.d_ctl->pending, 0, sizeof(uint32_t), stream) != hipSuccess) return -EIO;
-#ifdef SR_PERSIST_KERNEL
-    if constexpr ((ABL & KV_PERSIST) != 0) {
-        // one workgroup per resident slot (4 per CU), the scanners' slots included: per XCD class the
-        // slots of its XCD less the scanners placed there (block b runs on XCD b % 8)
-        if (!ds.persist_slots) {
-            int occ = 0, cus = 0, dev = 0;
-            (void)hipGetDevice(&dev);
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, (const void *)route_persist_kernel<ABL>, BLOCK, 0) !=
-                    hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || occ <= 0 ||
-                cus <= 0)
-                return -EIO;
-            ds.persist_slots = (uint32_t)(occ * cus);
-        }
-        uint32_t workers;
-        if (xl) {
-            const uint32_t per_xcd = ds.persist_slots / 8u, scan_xcd = (p.nb + 7u) / 8u;
-            p.pworkers = per_xcd > scan_xcd + 1u ? per_xcd - scan_xcd : 1u;
-            workers = 8u * p.pworkers;
-        } else {
-            p.pworkers = ds.persist_slots > p.nb + 1u ? ds.persist_slots - p.nb : 1u;
-            workers = p.pworkers;
-        }
-        p.total_blocks = p.nb + workers;
-        hipLaunchKernelGGL((route_persist_kernel<ABL>), dim3(p.total_blocks), dim3(BLOCK), 0, stream, p);
-    } else
-#endif
     // Route + pack with every dead first pick deferred and at most kOverlay dead (no wide probes), at most
     // 1024 shards: the packing's counting pass runs the deferred probes (no probe_defer_kernel)
     const bool fused = ds.fuse_defer && p.defer && p.picks == 1 && !p.mark_tiles && ds.dead <= (uint32_t)kOverlay &&

@@ -160,8 +160,6 @@ struct Control {
     uint32_t layout[8][32];  // KV_SEGMENTS launches, sharded: [0] tiles that weighed the segment
                              // layout, [1] tiles it saves two or more rounds (published per launch
                              // by the last block)
-    uint32_t ptile[8][32];   // route_persist_kernel: per XCD class, the next tile to take (reset by
-                             // the last block)
 };
 
 // One batch of a launch. A launch routes up to kMaxBatches independent batches: tiles
@@ -220,7 +218,7 @@ struct RouteParams {
     const uint64_t *cpow;
     uint64_t *tail;
     uint32_t lb_spin;
-    uint32_t pworkers;       // route_persist_kernel: workgroups per XCD class (persist_kernel.hpp)
+    uint32_t pad_lb;
     // route_chunk_kernel (SR_KNOB_PREFETCH): a tile workgroup also touches one dword per 128-byte line of
     // the tile `prefetch` tiles further on in its batch (the one its XCD runs about that many tiles
     // later), so that tile's loads find it in L2 / the memory-side cache; 0: off
@@ -1267,7 +1265,6 @@ __device__ void arrive(const RouteParams &p, uint32_t blk, uint32_t epoch) {
         __hip_atomic_store(&p.ctl->done[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         weighed += __hip_atomic_exchange(&p.ctl->layout[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         segmented += __hip_atomic_exchange(&p.ctl->layout[s8][1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&p.ctl->ptile[s8][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (weighed && p.layout_out) {   // the host's layout choice reads these (route_host.hpp)
         __hip_atomic_store(&p.layout_out[1], weighed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1280,15 +1277,14 @@ __device__ void arrive(const RouteParams &p, uint32_t blk, uint32_t epoch) {
 template <int BLOCK, unsigned ABL>
 struct KernelTraits {
     // waves per SIMD to reserve registers for: 1024-thread tiles run one workgroup per CU,
-    // smaller tiles several (LDS: 86 KB / 45 KB / 24 KB per workgroup); persistent workgroups
-    // hold a second tile in registers and hide latency by prefetch instead of occupancy
+    // smaller tiles several (LDS: 86 KB / 45 KB / 24 KB per workgroup)
     static constexpr int kMinWavesPerSimd = BLOCK >= 1024 ? 4 : (BLOCK >= 512 ? 6 : 7);
     static constexpr int kMaxWavesPerSimd = 8;
     static constexpr int kMaxVgpr = 512 / kMinWavesPerSimd / 8 * 8;   // 72 for 7 waves per SIMD
 };
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, never for its
-// outstanding global loads (a persistent workgroup keeps the next tile's loads in flight across it).
+// outstanding global loads.
 __device__ __forceinline__ void wg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // The batch of tile ci of XCD class cls (>= kMaxBatches: a padding block) and the tile's index

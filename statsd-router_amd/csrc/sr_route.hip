@@ -48,7 +48,7 @@ struct sr_ctx {
     // sr_pack_owner_sizes / sr_pack_owner_scatter: the split sizes of the pack in progress, and where its
     // scatter wrote owner `own`'s chunk (sr_exchange_data then skips that chunk's copy)
     uint64_t *own_counts;
-    uint64_t own_shape;   // n_owners and the batches' tile count of that pack (the scatter must match)
+    uint64_t own_shape;   // key of that pack's batches and owners (pack_shape; the scatter must match)
     int own_set, own;
     uint8_t *own_bytes;
     sr_record *own_recs;
@@ -97,13 +97,6 @@ static void free_ptr(void *p) { (void)hipFree(p); }
 // never the shipped library): SR_VARIANT in the environment then selects one.
 static int launch_product(DeviceState &ds, const RouteParams &p, hipStream_t stream) {
     const bool seg = ds.choose_segments(stream);
-#ifdef SR_PERSIST_KERNEL
-    // every shard alive, persistent chunk kernel asked for (SR_KNOB_PERSIST; developer builds)
-    if (ds.dead == 0 && ds.persist && !seg && (ds.persist == 2 || ds.last_layout == SR_LAYOUT_CHUNKS)) {
-        ds.last_layout = SR_LAYOUT_CHUNKS;
-        return launch_route<kBlock, KV_CHUNKS | KV_ALIVE | KV_PERSIST>(ds, p, stream);
-    }
-#endif
     if (ds.last_layout == SR_LAYOUT_CHUNKS) {
         if (ds.dead == 0) return launch_route<kBlock, KV_CHUNKS | KV_ALIVE | SR_CHUNK_ABL>(ds, p, stream);
         return launch_route<kBlock, KV_CHUNKS | SR_CHUNK_ABL>(ds, p, stream);
@@ -283,14 +276,6 @@ int sr_set_knob(sr_ctx *c, int knob, int64_t v) {
         if (v != 0 && v != kMtuChunkSmall && v != kMtuChunk) return -EINVAL;
         c->mtu_chunk = (uint32_t)v;
         return 0;
-    case SR_KNOB_PERSIST:
-#ifdef SR_PERSIST_KERNEL
-        if (v < 0 || v > 2) return -EINVAL;
-        c->ds.persist = (uint32_t)v;
-        return 0;
-#else
-        return v == 0 ? 0 : -ENOTSUP;   // the kernel is in developer builds only (`make VARIANTS=1`)
-#endif
     case SR_KNOB_MTU_XCD:
     case SR_KNOB_MTU_WALK:
     case SR_KNOB_HIST:
@@ -418,10 +403,22 @@ int sr_pack_by_owner(sr_ctx *c, const uint8_t *d_bytes, size_t nbytes, const sr_
     return pack_launch(c, &b, 1, n_owners, d_out_bytes, out_cap, d_out_recs, d_owner_counts);
 }
 
+// The key sr_pack_owner_scatter must match: the batch descriptors (pointers, sizes) and owners of the
+// context's last sr_pack_owner_sizes, whose tile bases and split sizes the scatter uses (FNV-1a)
 static uint64_t pack_shape(const PackBatch *in, size_t count, uint32_t n_owners) {
-    uint64_t tiles = 0;
-    for (size_t j = 0; j < count; ++j) tiles += (in[j].max_records + kPackTile - 1) / kPackTile;
-    return tiles << 8 | n_owners;
+    uint64_t h = 0xcbf29ce484222325ull;
+    auto mix = [&h](uint64_t v) {
+        for (int i = 0; i < 8; ++i, v >>= 8) h = (h ^ (v & 0xFFu)) * 0x100000001b3ull;
+    };
+    mix(n_owners);
+    mix(count);
+    for (size_t j = 0; j < count; ++j) {
+        mix((uint64_t)(uintptr_t)in[j].bytes);
+        mix((uint64_t)(uintptr_t)in[j].recs);
+        mix((uint64_t)(uintptr_t)in[j].n_records);
+        mix((uint64_t)in[j].nbytes << 32 | in[j].max_records);
+    }
+    return h;
 }
 
 static int pack_many_args(const sr_batch *batches, size_t count, uint32_t n_owners, PackBatch *in,
@@ -473,7 +470,7 @@ int sr_pack_owner_sizes(sr_ctx *c, const sr_batch *batches, size_t count, uint32
 int sr_pack_owner_scatter(sr_ctx *c, const sr_batch *batches, size_t count, uint32_t n_owners, int own,
                           uint8_t *d_own_bytes, sr_record *d_own_recs, uint8_t *d_out_bytes, size_t out_cap,
                           sr_record *d_out_recs) {
-    if (!c || !c->own_counts || own < 0 || (uint32_t)own >= n_owners) return -EINVAL;
+    if (!c || !c->own_counts || own < -1 || own >= (int)n_owners) return -EINVAL;
     uint64_t total_bytes = 0;
     PackBatch in[kPackMaxBatches];
     int rc = pack_many_args(batches, count, n_owners, in, &total_bytes);
@@ -481,10 +478,11 @@ int sr_pack_owner_scatter(sr_ctx *c, const sr_batch *batches, size_t count, uint
     if (pack_shape(in, count, n_owners) != c->own_shape) return -EINVAL;
     if (out_cap < SR_PACK_CAPACITY(total_bytes)) return -EINVAL;
     if (out_cap > 0xFFFFFFFFull) out_cap = 0xFFFFFFFFull;
-    if (!d_out_bytes || !d_out_recs || !d_own_bytes || !d_own_recs || ((uintptr_t)d_own_bytes & 3u)) return -EINVAL;
+    if (!d_out_bytes || !d_out_recs) return -EINVAL;
+    if (own >= 0 && (!d_own_bytes || !d_own_recs || ((uintptr_t)d_own_bytes & 3u))) return -EINVAL;
     (void)hipSetDevice(c->device);
     // sr_exchange_data finds the own chunk in place and does not copy it
-    c->own_set = 1;
+    c->own_set = own >= 0;
     c->own = own;
     c->own_bytes = d_own_bytes;
     c->own_recs = d_own_recs;
@@ -1149,6 +1147,7 @@ struct RcclTransport {
     RcclApi *r;
     sr_comm *comm;
     hipStream_t stream;
+    sr_ctx *ctx;
 };
 
 static int rccl_group_start(void *u) { return ((RcclTransport *)u)->r->group_start() == 0 ? 0 : -EIO; }
@@ -1176,7 +1175,7 @@ int sr_exchange_data(sr_ctx *ctx, sr_comm *comm, const uint8_t *d_packed, const 
     RcclApi *r = rccl_api();
     if (!r) return -ENOSYS;
     (void)hipSetDevice(ctx->device);
-    RcclTransport rt{r, comm, ctx->stream};
+    RcclTransport rt{r, comm, ctx->stream, ctx};
     const sr_transport t{&rt, rccl_group_start, rccl_group_end, rccl_send, rccl_recv, rccl_copy, rccl_rebase};
     // the own chunk already in its place (sr_pack_owner_scatter into these receive buffers): no copy
     bool in_place = false;
@@ -1193,26 +1192,65 @@ int sr_exchange_data(sr_ctx *ctx, sr_comm *comm, const uint8_t *d_packed, const 
                         d_recv_recs, in_place);
 }
 
+// One route launch's regroup on any transport (sr_regroup_run): the split sizes, the size exchange
+// (the one host round trip), the plan, the scatter with the rank's own chunk written straight into its
+// place in the receive buffers, then the exchange without the own chunk's copy and the rebase.
+// sr_regroup_launch is this on RCCL: both run this one sequence.
+static int regroup_run(sr_ctx *ctx, const sr_transport &t, sr_sizes_fn sizes, int world, int rank,
+                       const sr_batch *batches, size_t count, uint64_t *d_owner_counts, uint64_t *d_recv_counts,
+                       uint8_t *d_packed, size_t packed_cap, sr_record *d_packed_recs, uint8_t *d_recv_bytes,
+                       size_t recv_bytes_cap, sr_record *d_recv_recs, size_t recv_recs_cap, uint64_t *h_sent,
+                       uint64_t *h_received) {
+    if (!ctx || !sizes || !d_owner_counts || !d_recv_counts || !d_recv_bytes || !d_recv_recs || !h_sent ||
+        !h_received || world < 1 || world > (int)kMaxOwners || rank < 0 || rank >= world)
+        return -EINVAL;
+    int rc = sr_pack_owner_sizes(ctx, batches, count, (uint32_t)world, d_owner_counts);
+    if (rc) return rc;
+    if ((rc = sizes(t.user, d_owner_counts, d_recv_counts, h_sent, h_received))) return rc;
+    sr_exchange_peer peers[kMaxOwners];
+    uint64_t tot[4];
+    if ((rc = exchange_plan(world, rank, h_sent, h_received, peers, tot))) return rc;
+    if (tot[2] > recv_recs_cap || tot[3] > recv_bytes_cap) return -ENOSPC;
+    const sr_exchange_peer &e = peers[rank];
+    rc = sr_pack_owner_scatter(ctx, batches, count, (uint32_t)world, rank, d_recv_bytes + e.recv_byte0,
+                               d_recv_recs + e.recv_line0, d_packed, packed_cap, d_packed_recs);
+    ctx->own_set = 0;   // consumed here: the exchange below is told the own chunk is in place
+    if (rc) return rc;
+    return exchange_run(t, world, rank, h_sent, h_received, d_packed, d_packed_recs, d_recv_bytes, d_recv_recs,
+                        true);
+}
+
+static int rccl_sizes(void *u, const uint64_t *d_owner_counts, uint64_t *d_recv_counts, uint64_t *h_sent,
+                      uint64_t *h_received) {
+    RcclTransport *t = (RcclTransport *)u;
+    return sr_exchange_sizes(t->ctx, t->comm, d_owner_counts, d_recv_counts, h_sent, h_received);
+}
+
 int sr_regroup_launch(sr_ctx *ctx, sr_comm *comm, const sr_batch *batches, size_t count,
                       uint64_t *d_owner_counts, uint64_t *d_recv_counts, uint8_t *d_packed, size_t packed_cap,
                       sr_record *d_packed_recs, uint8_t *d_recv_bytes, size_t recv_bytes_cap,
                       sr_record *d_recv_recs, size_t recv_recs_cap, uint64_t *h_sent, uint64_t *h_received) {
-    if (!ctx || !comm || !d_recv_bytes || !d_recv_recs || !h_sent || !h_received) return -EINVAL;
-    const uint32_t world = (uint32_t)comm->world;
-    int rc = sr_pack_owner_sizes(ctx, batches, count, world, d_owner_counts);
-    if (rc) return rc;
-    rc = sr_exchange_sizes(ctx, comm, d_owner_counts, d_recv_counts, h_sent, h_received);
-    if (rc) return rc;
-    sr_exchange_peer peers[kMaxOwners];
-    uint64_t tot[4];
-    rc = exchange_plan(comm->world, comm->rank, h_sent, h_received, peers, tot);
-    if (rc) return rc;
-    if (tot[2] > recv_recs_cap || tot[3] > recv_bytes_cap) return -ENOSPC;
-    const sr_exchange_peer &e = peers[comm->rank];
-    rc = sr_pack_owner_scatter(ctx, batches, count, world, comm->rank, d_recv_bytes + e.recv_byte0,
-                               d_recv_recs + e.recv_line0, d_packed, packed_cap, d_packed_recs);
-    if (rc) return rc;
-    return sr_exchange_data(ctx, comm, d_packed, d_packed_recs, h_sent, h_received, d_recv_bytes, d_recv_recs);
+    if (!ctx || !comm) return -EINVAL;
+    RcclApi *r = rccl_api();
+    if (!r) return -ENOSYS;
+    (void)hipSetDevice(ctx->device);
+    RcclTransport rt{r, comm, ctx->stream, ctx};
+    const sr_transport t{&rt, rccl_group_start, rccl_group_end, rccl_send, rccl_recv, rccl_copy, rccl_rebase};
+    return regroup_run(ctx, t, rccl_sizes, comm->world, comm->rank, batches, count, d_owner_counts, d_recv_counts,
+                       d_packed, packed_cap, d_packed_recs, d_recv_bytes, recv_bytes_cap, d_recv_recs, recv_recs_cap,
+                       h_sent, h_received);
+}
+
+int sr_regroup_run(sr_ctx *ctx, const sr_transport *t, sr_sizes_fn sizes, int world, int rank,
+                   const sr_batch *batches, size_t count, uint64_t *d_owner_counts, uint64_t *d_recv_counts,
+                   uint8_t *d_packed, size_t packed_cap, sr_record *d_packed_recs, uint8_t *d_recv_bytes,
+                   size_t recv_bytes_cap, sr_record *d_recv_recs, size_t recv_recs_cap, uint64_t *h_sent,
+                   uint64_t *h_received) {
+    if (!ctx || !t) return -EINVAL;
+    (void)hipSetDevice(ctx->device);
+    return regroup_run(ctx, *t, sizes, world, rank, batches, count, d_owner_counts, d_recv_counts, d_packed,
+                       packed_cap, d_packed_recs, d_recv_bytes, recv_bytes_cap, d_recv_recs, recv_recs_cap, h_sent,
+                       h_received);
 }
 
 int sr_exchange_plan(int world, int rank, const uint64_t *h_sent, const uint64_t *h_received,

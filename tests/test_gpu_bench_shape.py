@@ -181,30 +181,6 @@ def test_chunk_layout_32_batch_launch_c5(pkg, oracle, dead):
         assert got[b]["fill_out"].tolist() == fo_o.tolist(), b
 
 
-@pytest.mark.parametrize("cfg,nb", [("c2", 32), ("c5", 32), ("c3", 9), ("c4", 8), ("c2", 3)])
-def test_persist_kernel_launch_shapes(pkg, oracle, cfg, nb):
-    """route_persist_kernel (SR_KNOB_PERSIST 2, every shard alive) on bench.py's launch shapes: every
-    batch's records against the oracle, then packed in the same sr_pack_packets_many."""
-    _, _, _, n, _, _ = _cfg(cfg)
-    alive = [1] * n
-    streams = _streams(pkg, cfg, nb)
-    fills = np.random.default_rng(77 + nb).integers(0, 1451, (nb, n))
-    with pkg.Router(n, 1 << 16) as r:
-        try:
-            r.set_knob(pkg.SR_KNOB_PERSIST, 2)
-        except pkg.SrError as e:
-            pytest.skip(f"route_persist_kernel not in this build ({e})")
-    got, layout = _route_pack_many(pkg, streams, n, alive, fills, layout=3, knobs=[(pkg.SR_KNOB_PERSIST, 2)])
-    assert layout == 3
-    for b, s in enumerate(streams):
-        recs, cnt, probed = _oracle_route(oracle, cfg, False, b, s, n, alive)
-        assert got[b]["n_lines"] == cnt, b
-        assert np.array_equal(got[b]["recs"], recs), f"batch {b}: persistent-kernel records differ"
-        srt_o, pk_o, fo_o, _ = oracle.pack_packets(recs, n, fills[b], probed)
-        assert np.array_equal(got[b]["packets"].view(np.uint8), pk_o.view(np.uint8)), b
-        assert got[b]["fill_out"].tolist() == fo_o.tolist(), b
-
-
 def test_route_pack_many_shapes(pkg, oracle):
     """sr_route_pack_many on shapes its tile-histogram sort must get right: tiles of 2,700 six-byte
     lines (several 1024-record rounds per group of tiles), empty and one-line batches, 16 shards (the

@@ -151,49 +151,3 @@ def test_chunks_tile_straddles_and_lookback(pkg, oracle, spin):
                              f"{name} chunks N={n} dead={dead} spin={spin}")
         finally:
             r.close()
-
-
-PERSIST = 2   # SR_KNOB_PERSIST: every all-alive launch on route_persist_kernel
-
-
-def _persist_or_skip(pkg, r):
-    """route_persist_kernel is built into developer libraries only (make VARIANTS=1, SR_ROUTE_LIB)."""
-    try:
-        r.set_knob(pkg.SR_KNOB_PERSIST, PERSIST)
-    except pkg.SrError as e:
-        r.close()
-        pytest.skip(f"route_persist_kernel not in this build ({e})")
-
-
-@pytest.mark.parametrize("n", [4, 64, 7])
-@pytest.mark.parametrize("spin", [None, 0])
-def test_persist_kernel_matches_oracle(pkg, oracle, n, spin):
-    """route_persist_kernel (persistent workgroups, LDS-DMA double buffer; every shard alive) on the
-    layout streams, the tile-straddle shapes, with and without the look-back fallback (spin 0)."""
-    rng = np.random.default_rng(21)
-    r = pkg.Router(n, 4 << 20)
-    try:
-        _persist_or_skip(pkg, r)
-        if spin is not None:
-            r.set_knob(pkg.SR_KNOB_LB_SPIN, spin)
-        for name, data in list(_streams(pkg)) + [("straddles", _tile_straddles(rng))]:
-            _assert_same(r.route(data, want_hashes=True), oracle.route(data, n, None), f"{name} persist N={n} spin={spin}")
-            assert r.last_layout() in (CHUNKS, SEGMENTS)   # (AUTO's first launch is a segment probe)
-    finally:
-        r.close()
-
-
-def test_persist_full_size_digests(pkg):
-    """The 16 MiB configuration digests (C2..C5, every shard alive) on route_persist_kernel."""
-    for key, d in sorted(load_digests().items()):
-        if not key.endswith("/all"):
-            continue
-        s = pkg.gen_stream(d["nbytes"], d["line_lens"], seed=d["seed"], p_invalid=d["p_invalid"])
-        r = pkg.Router(d["n_downstreams"], d["nbytes"])
-        try:
-            _persist_or_skip(pkg, r)
-            recs, hs, cnt = r.route(s.data, want_hashes=True)
-        finally:
-            r.close()
-        assert cnt == d["n_lines"], key
-        assert hashlib.sha256(recs.tobytes()).hexdigest() == d["sha256_records"], key

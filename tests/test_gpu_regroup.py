@@ -555,3 +555,255 @@ def test_c_exchange_own_chunk_in_place(pkg, oracle, torch_stream):
     assert np.array_equal(got_b[:n_b], eb) and (got_b[n_b:] == 0xCD).all()
     assert np.array_equal(rr.cpu().numpy().view(pkg.RECORD_DTYPE), er)
     assert (d_pb.cpu().numpy() == 0xAB).all()   # the packed buffer was never needed
+
+
+def _rank_inputs(pkg, oracle, rank, world, n_shards, nb=2):
+    """Per-rank launch inputs of the multi-rank regroup tests: rank 0 has nothing valid (source 0 sends
+    nothing, so every owner's first chunk is empty and its rebase starts past line 0); rank 1 routes with
+    the shards it owns dead, so its own chunk is empty while the others send to it; the rest are mixed
+    lengths with invalid lines and a few dead shards. Every batch's last line is a valid line ending at
+    the batch's last byte (the owner scatter's piece that crosses the batch's end), the batch sizes
+    varying mod 4."""
+    if rank == 1 % world:
+        alive = [int(k % world != 1 % world or world == 1) for k in range(n_shards)]
+    else:
+        alive = [int(k % 7 != 3) for k in range(n_shards)]
+    datas = []
+    for b in range(nb):
+        if rank == 0 and world > 1:
+            d = np.frombuffer(pkg.frame_datagrams([b"no colon here\n", b"x\n", b"AAAA" * 300]), dtype=np.uint8)
+        else:
+            d = pkg.gen_stream((1 << 17) + 4099 * rank + 1001 * b, [64, 256, 1024], seed=1700 + 17 * rank + b,
+                               p_invalid=0.1).data
+            tail = (b"tail.%d.%d:1|c" % (rank, b)) + b"z" * ((rank + b) % 4)
+            d = np.concatenate([d, np.frombuffer(pkg.frame_datagrams([tail]), dtype=np.uint8)])
+        datas.append(np.ascontiguousarray(d))
+    recs = [oracle.route(d, n_shards, alive)[0] for d in datas]
+    return datas, recs, alive
+
+
+def _expected_receive(oracle, inputs, world, r):
+    """Owner r's receive buffer: every source's chunk r of its oracle pack, source by source, with the
+    records rebased into the concatenated bytes."""
+    packs = [oracle.pack_many_by_owner(d, rc, world) for d, rc, _ in inputs]
+    eb = np.concatenate([pb[int(cnt[:r, 1].sum()):][: int(cnt[r, 1])] for pb, pr, cnt in packs]) if packs else b""
+    er, base = [], 0
+    for pb, pr, cnt in packs:
+        x = pr[int(cnt[:r, 0].sum()):][: int(cnt[r, 0])].copy()
+        x["offset"] += np.uint32(base)
+        er.append(x)
+        base += int(cnt[r, 1])
+    return np.asarray(eb, dtype=np.uint8), np.concatenate(er), np.stack([p[2][r] for p in packs])
+
+
+@pytest.mark.parametrize("world,n_shards", [(2, 64), (3, 16), (8, 64), (3, 1)])
+def test_regroup_run_device_ranks(pkg, oracle, world, n_shards):
+    """sr_regroup_run — the sequence sr_regroup_launch runs on RCCL (pack sizes, size exchange, plan, own
+    chunk scattered into its place in the receive buffers, exchange without the own chunk's copy, rebase)
+    — with `world` ranks as threads of one process on one GPU, each its own context and stream, on a
+    mailbox transport over device memory. Every rank's receive bytes, rebased records and received sizes
+    equal the oracle's per-owner stream; the transport is never asked to copy the own chunk. Two
+    launches per rank (the context's pack state reused); rank 0 sends nothing, rank 1's own chunk is
+    empty; the last rank's first launch has receive buffers one line short (-ENOSPC) and finishes with
+    sr_pack_owner_scatter (own -1) + sr_exchange_run while its peers' sends wait."""
+    import ctypes
+    import threading
+
+    import torch
+
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    hip.hipMemcpy.restype = ctypes.c_int
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    D2H, H2D, D2D = 2, 1, 3
+    inputs = [_rank_inputs(pkg, oracle, r, world, n_shards) for r in range(world)]
+    box, cond, out, errs = {}, threading.Condition(), {}, {}
+
+    class Mailbox(pkg.Transport):
+        def __init__(self, rank, router):
+            self.rank, self.router, self.posted, self.step, self.calls = rank, router, [], 0, []
+
+        def _put(self, key, blob):
+            with cond:
+                box.setdefault(key, []).append(blob)
+                cond.notify_all()
+
+        def _take(self, key):
+            with cond:
+                assert cond.wait_for(lambda: box.get(key), timeout=90), key
+                return box[key].pop(0)
+
+        def sizes(self, d_cnt, d_rcv):
+            self.calls.append("sizes")
+            self.router.sync()
+            sent = np.zeros((world, 2), np.uint64)
+            assert hip.hipMemcpy(sent.ctypes.data, d_cnt, sent.nbytes, D2H) == 0
+            for q in range(world):
+                self._put(("sz", self.step, self.rank, q), sent[q].copy())
+            received = np.stack([self._take(("sz", self.step, q, self.rank)) for q in range(world)])
+            assert hip.hipMemcpy(d_rcv, received.ctypes.data, received.nbytes, H2D) == 0
+            self.step += 1
+            return sent, received
+
+        def group_start(self):
+            self.router.sync()   # the scatter wrote the packed chunks
+            self.posted = []
+
+        def send(self, addr, n, peer, tag):
+            self.calls.append(("send", peer, tag))
+            blob = ctypes.create_string_buffer(n)
+            assert hip.hipMemcpy(ctypes.addressof(blob), addr, n, D2H) == 0
+            self._put(("d", self.rank, peer, tag), blob)
+
+        def recv(self, addr, n, peer, tag):
+            self.calls.append(("recv", peer, tag))
+            self.posted.append((addr, n, peer, tag))
+
+        def group_end(self):
+            for addr, n, peer, tag in self.posted:
+                blob = self._take(("d", peer, self.rank, tag))
+                assert len(blob) == n and hip.hipMemcpy(addr, ctypes.addressof(blob), n, H2D) == 0
+
+        def copy(self, dst, src, n):
+            self.calls.append("copy")
+            assert hip.hipMemcpy(dst, src, n, D2D) == 0
+
+        def rebase(self, recs_addr, peers, n_lines):
+            self.router.exchange_rebase(recs_addr, peers)
+            self.router.sync()
+
+    def rank_main(r):
+        try:
+            torch.cuda.set_device(0)
+            datas, _, alive = inputs[r]
+            nb = len(datas)
+            cap = max(d.size for d in datas)
+            d_in = torch.zeros((nb, cap), dtype=torch.uint8, device="cuda")
+            for b, d in enumerate(datas):
+                d_in[b, : d.size].copy_(torch.from_numpy(d))
+            d_rec = torch.zeros((nb, cap), dtype=torch.int64, device="cuda")
+            d_n = torch.zeros(nb, dtype=torch.int64, device="cuda")
+            total = sum(int(d.size) for d in datas)
+            pcap = pkg.pack_capacity(total)
+            packed = torch.zeros(pcap, dtype=torch.uint8, device="cuda")
+            precs = torch.zeros(nb * cap, dtype=torch.int64, device="cuda")
+            counts = torch.zeros((world, 2), dtype=torch.int64, device="cuda")
+            rcv = torch.zeros((world, 2), dtype=torch.int64, device="cuda")
+            eb, er, ec = _expected_receive(oracle, inputs, world, r)
+            torch.cuda.synchronize()
+            got = []
+            with pkg.Router(n_shards, cap) as router:
+                router.set_alive(alive)
+                batches = [(d_in[b].data_ptr(), int(d.size), d_rec[b].data_ptr(), cap, d_n[b].data_ptr())
+                           for b, d in enumerate(datas)]
+                router.route_device_many([(db, n, dr, mr, None, dn) for db, n, dr, mr, dn in batches])
+                t = Mailbox(r, router)
+                for step in range(2):
+                    short = step == 0 and r == world - 1 and world > 1 and len(er) > 0
+                    nl = max(len(er) - (1 if short else 0), 1)
+                    rb = torch.full((eb.size + 64,), 0xCD, dtype=torch.uint8, device="cuda")
+                    rr = torch.full((nl,), -1, dtype=torch.int64, device="cuda")
+                    torch.cuda.synchronize()
+                    fits, sent, received = router.regroup_run(
+                        t, world, r, batches, counts.data_ptr(), rcv.data_ptr(), packed.data_ptr(), pcap,
+                        precs.data_ptr(), rb.data_ptr(), rb.numel(), rr.data_ptr(), nl)
+                    assert fits == (not short), (r, step, fits)
+                    if not fits:   # finish: everything packed, then the exchange with the own chunk copied
+                        rr = torch.full((len(er),), -1, dtype=torch.int64, device="cuda")
+                        torch.cuda.synchronize()
+                        router.pack_owner_scatter(batches, world, -1, 0, 0, packed.data_ptr(), pcap,
+                                                  precs.data_ptr())
+                        pkg.exchange_run(t, world, r, sent, received, packed.data_ptr(), precs.data_ptr(),
+                                         rb.data_ptr(), rr.data_ptr())
+                    router.sync()
+                    got.append((rb.cpu().numpy(), rr.cpu().numpy().view(pkg.RECORD_DTYPE)[: len(er)],
+                                received.astype(np.int64), rcv.cpu().numpy(), fits))
+            out[r] = (got, eb, er, ec, t.calls)
+        except Exception as e:   # noqa: BLE001
+            import traceback
+            errs[r] = traceback.format_exc()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(240)
+    assert not any(t.is_alive() for t in th), "a rank did not finish"
+    assert not errs, "\n".join(f"rank {r}:\n{e}" for r, e in errs.items())
+    for r in range(world):
+        got, eb, er, ec, calls = out[r]
+        for step, (rb, rr, received, rcv, fits) in enumerate(got):
+            assert received.tolist() == ec.tolist() == rcv.tolist(), (r, step)
+            assert np.array_equal(rb[: eb.size], eb), (r, step)
+            assert (rb[eb.size:] == 0xCD).all(), (r, step)
+            assert np.array_equal(rr, er), (r, step)
+        # the own chunk is never copied by the one-call sequence (only by the -ENOSPC fallback)
+        fell_back = any(not g[4] for g in got)
+        assert calls.count("copy") == (2 if fell_back and ec[r, 0] else 0), calls
+        assert all(c[1] != r for c in calls if isinstance(c, tuple)), "a send or recv to itself"
+
+
+def _end_straddle_batches(pkg):
+    """Batches whose valid last line ends at the batch's last byte, for every (line start % 4,
+    nbytes % 4) and several last-line lengths (one to five 16-byte pieces): the owner scatter's piece
+    that crosses the batch's end must come out byte-exact."""
+    out = []
+    for a in range(4):
+        for b in range(4):
+            first = b"first.%d%d" % (a, b)
+            first += b"x" * ((a - 1 - len(first) - 4) % 4) + b":1|c"   # framed: len + 1 = a (mod 4)
+            L = 24 + 16 * ((a + b) % 5) + ((b - a) % 4) + 4 * (a & 1)        # framed length = b - a (mod 4)
+            body = b"last.%d.%d." % (a, b)
+            last = body + b"y" * (L - 1 - len(body) - 4) + b":1|c"
+            d = np.frombuffer(pkg.frame_datagrams([first, last]), dtype=np.uint8)
+            assert (len(first) + 1) % 4 == a and d.size % 4 == b and d[-1] == 10
+            out.append(np.ascontiguousarray(d))
+    return out
+
+
+@pytest.mark.parametrize("G,own", [(2, None), (2, 0), (3, 1), (1, 0)])
+def test_owner_scatter_batch_end_piece(pkg, oracle, G, own, torch_stream):
+    """The owner pack of 16 batches whose last line ends at the batch's end (every line start % 4 and
+    nbytes % 4): packed bytes and records equal the oracle's, also with one owner's chunk scattered into
+    its own buffer."""
+    import torch
+
+    datas = _end_straddle_batches(pkg)
+    nb, n_shards = len(datas), 4
+    cap = max(d.size for d in datas)
+    d_in = torch.zeros((nb, cap), dtype=torch.uint8, device="cuda")
+    for b, d in enumerate(datas):
+        d_in[b, : d.size].copy_(torch.from_numpy(d))
+    d_rec = torch.zeros((nb, cap), dtype=torch.int64, device="cuda")
+    d_n = torch.zeros(nb, dtype=torch.int64, device="cuda")
+    total = sum(int(d.size) for d in datas)
+    pcap = pkg.pack_capacity(total)
+    d_pb = torch.full((pcap,), 0xAB, dtype=torch.uint8, device="cuda")
+    d_pr = torch.full((nb * cap,), -1, dtype=torch.int64, device="cuda")
+    d_cnt = torch.zeros((G, 2), dtype=torch.int64, device="cuda")
+    recs_list = [oracle.route(d, n_shards)[0] for d in datas]
+    eb, er, ec = oracle.pack_many_by_owner(datas, recs_list, G)
+    batches = [(d_in[b].data_ptr(), int(d.size), d_rec[b].data_ptr(), cap, d_n[b].data_ptr()) for b, d in enumerate(datas)]
+    with pkg.Router(n_shards, cap) as r:
+        r.set_stream(torch_stream.cuda_stream)
+        r.route_device_many([(db, n, dr, mr, None, dn) for db, n, dr, mr, dn in batches])
+        if own is None:
+            r.pack_many_by_owner(batches, G, d_pb.data_ptr(), pcap, d_pr.data_ptr(), d_cnt.data_ptr())
+        else:
+            r.pack_owner_sizes(batches, G, d_cnt.data_ptr())
+            ob = torch.full((int(ec[own, 1]) + 64,), 0xCD, dtype=torch.uint8, device="cuda")
+            orr = torch.full((int(ec[own, 0]) + 1,), -1, dtype=torch.int64, device="cuda")
+            r.pack_owner_scatter(batches, G, own, ob.data_ptr(), orr.data_ptr(), d_pb.data_ptr(), pcap, d_pr.data_ptr())
+        torch_stream.synchronize()
+    assert d_cnt.cpu().numpy().tolist() == ec.tolist()
+    l0 = np.concatenate([[0], np.cumsum(ec[:, 0])]).astype(np.int64)
+    b0 = np.concatenate([[0], np.cumsum(ec[:, 1])]).astype(np.int64)
+    got_b = d_pb.cpu().numpy()
+    got_r = np.frombuffer(d_pr.cpu().numpy().tobytes(), dtype=pkg.RECORD_DTYPE)
+    for o in range(G):
+        if o == own:
+            mine_b, mine_r = ob.cpu().numpy(), orr.cpu().numpy()
+            assert np.array_equal(mine_b[: ec[o, 1]], eb[b0[o]: b0[o + 1]]) and (mine_b[ec[o, 1]:] == 0xCD).all()
+            assert np.array_equal(mine_r[: ec[o, 0]].view(pkg.RECORD_DTYPE), er[l0[o]: l0[o + 1]])
+        else:
+            assert np.array_equal(got_b[b0[o]: b0[o + 1]], eb[b0[o]: b0[o + 1]]), o
+            assert np.array_equal(got_r[l0[o]: l0[o + 1]], er[l0[o]: l0[o + 1]]), o

@@ -197,3 +197,136 @@ def test_comm_from_group_gloo(fail):
             assert "sr_comm_id" in res[r]["error"]
         else:
             assert res[r] == {"id": b"\x01" * 128, "world": world, "rank": r, "device": 3}
+
+
+def _gpu_regroup_worker(rank, world, port, n_shards, q):
+    """One rank of test_regroup_run_gloo_gpu: its own process and context on GPU 0, sr_regroup_run on a
+    gloo transport (device buffers staged through host tensors)."""
+    try:
+        sys.path.insert(0, REPO)
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import ctypes
+
+        import torch
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pkg = importlib.import_module("statsd-router_amd")
+        import sr_oracle as oracle
+        from test_gpu_regroup import _expected_receive, _rank_inputs
+
+        torch.cuda.set_device(0)
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        hip.hipMemcpy.restype = ctypes.c_int
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        D2H, H2D, D2D = 2, 1, 3
+
+        class GlooDevice(pkg.Transport):
+            def __init__(self, router):
+                self.router, self.pending, self.recvs, self.calls = router, [], [], []
+
+            def sizes(self, d_cnt, d_rcv):
+                self.router.sync()
+                sent = torch.zeros((world, 2), dtype=torch.int64)
+                assert hip.hipMemcpy(sent.data_ptr(), d_cnt, 16 * world, D2H) == 0
+                received = torch.empty_like(sent)
+                dist.all_to_all_single(received, sent)
+                assert hip.hipMemcpy(d_rcv, received.data_ptr(), 16 * world, H2D) == 0
+                return sent.numpy().astype(np.uint64), received.numpy().astype(np.uint64)
+
+            def group_start(self):
+                self.router.sync()
+                self.pending, self.recvs = [], []
+
+            def send(self, addr, n, peer, tag):
+                self.calls.append(("send", peer))
+                h = torch.empty(n, dtype=torch.uint8)
+                assert hip.hipMemcpy(h.data_ptr(), addr, n, D2H) == 0
+                self.pending.append((dist.isend(h, peer, tag=tag), h))
+
+            def recv(self, addr, n, peer, tag):
+                self.calls.append(("recv", peer))
+                h = torch.empty(n, dtype=torch.uint8)
+                self.pending.append((dist.irecv(h, peer, tag=tag), h))
+                self.recvs.append((addr, h))
+
+            def group_end(self):
+                for w, _ in self.pending:
+                    w.wait()
+                for addr, h in self.recvs:
+                    assert hip.hipMemcpy(addr, h.data_ptr(), h.numel(), H2D) == 0
+
+            def copy(self, dst, src, n):
+                self.calls.append("copy")
+                assert hip.hipMemcpy(dst, src, n, D2D) == 0
+
+            def rebase(self, recs_addr, peers, n_lines):
+                self.router.exchange_rebase(recs_addr, peers)
+                self.router.sync()
+
+        inputs = [_rank_inputs(pkg, oracle, r, world, n_shards) for r in range(world)]
+        datas, _, alive = inputs[rank]
+        eb, er, ec = _expected_receive(oracle, inputs, world, rank)
+        nb, cap = len(datas), max(d.size for d in datas)
+        d_in = torch.zeros((nb, cap), dtype=torch.uint8, device="cuda")
+        for b, d in enumerate(datas):
+            d_in[b, : d.size].copy_(torch.from_numpy(d))
+        d_rec = torch.zeros((nb, cap), dtype=torch.int64, device="cuda")
+        d_n = torch.zeros(nb, dtype=torch.int64, device="cuda")
+        pcap = pkg.pack_capacity(sum(int(d.size) for d in datas))
+        packed = torch.zeros(pcap, dtype=torch.uint8, device="cuda")
+        precs = torch.zeros(nb * cap, dtype=torch.int64, device="cuda")
+        counts = torch.zeros((world, 2), dtype=torch.int64, device="cuda")
+        rcv = torch.zeros((world, 2), dtype=torch.int64, device="cuda")
+        rb = torch.full((eb.size + 64,), 0xCD, dtype=torch.uint8, device="cuda")
+        rr = torch.full((max(len(er), 1),), -1, dtype=torch.int64, device="cuda")
+        torch.cuda.synchronize()
+        with pkg.Router(n_shards, cap) as router:
+            router.set_alive(alive)
+            batches = [(d_in[b].data_ptr(), int(d.size), d_rec[b].data_ptr(), cap, d_n[b].data_ptr())
+                       for b, d in enumerate(datas)]
+            router.route_device_many([(db, n, dr, mr, None, dn) for db, n, dr, mr, dn in batches])
+            t = GlooDevice(router)
+            fits, sent, received = router.regroup_run(t, world, rank, batches, counts.data_ptr(), rcv.data_ptr(),
+                                                      packed.data_ptr(), pcap, precs.data_ptr(), rb.data_ptr(),
+                                                      rb.numel(), rr.data_ptr(), rr.numel())
+            router.sync()
+        assert fits
+        assert received.astype(np.int64).tolist() == ec.tolist() == rcv.cpu().numpy().tolist()
+        got_b = rb.cpu().numpy()
+        assert np.array_equal(got_b[: eb.size], eb) and (got_b[eb.size:] == 0xCD).all()
+        assert np.array_equal(rr.cpu().numpy().view(pkg.RECORD_DTYPE)[: len(er)], er)
+        assert "copy" not in t.calls and all(c[1] != rank for c in t.calls if isinstance(c, tuple))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, None))
+    except Exception:
+        q.put((rank, traceback.format_exc()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,n_shards", [(2, 64), (3, 16)])
+def test_regroup_run_gloo_gpu(world, n_shards):
+    """sr_regroup_run (sr_regroup_launch's sequence) with `world` processes on one GPU over gloo: every
+    rank's receive bytes, rebased records and received sizes equal the oracle's per-owner stream, and the
+    own chunk is never copied (it is scattered into its place)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gpu_regroup_worker, args=(r, world, port, n_shards, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            rank, err = q.get(timeout=240)
+            res[rank] = err
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    errs = {r: e for r, e in res.items() if e}
+    assert not errs, "\n".join(f"rank {r}:\n{e}" for r, e in errs.items())
