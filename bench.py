@@ -85,6 +85,9 @@ def parse(argv=None):
                     help="developer A/B: pack the own chunk into the packed buffer and copy it (round-4 path)")
     ap.add_argument("--regroup-split-calls", action="store_true",
                     help="developer A/B: the regroup's calls one by one from Python instead of sr_regroup_launch")
+    ap.add_argument("--regroup-slots", type=int, default=2, choices=[1, 2],
+                    help="regroup steps alternating over this many contexts and streams (2: step i + 1's route "
+                         "overlaps step i's scatter and exchange)")
     ap.add_argument("--cpu-seconds", type=float, default=1.5)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
@@ -350,7 +353,8 @@ def main(argv=None):
         if not args.no_pack:
             result["route_pack"] = pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev,
                                             dead=sum(alive) < shards, alive=alive, threads=args.pack_threads,
-                                            host=None if args.no_verify else host, knobs=args.knob)
+                                            host=None if args.no_verify else host, knobs=args.knob,
+                                            min_warmup_ms=args.min_warmup_ms)
         if args.knob:
             result["config"]["knobs"] = args.knob
     router.close()
@@ -384,7 +388,8 @@ def main(argv=None):
         try:   # a failing regroup leg must not take the main line with it
             rg = regroup_leg(pkg, dev, local, world, rank, args.regroup_config, args.regroup_steps,
                              per_step=args.regroup_batches, exchange=args.exchange,
-                             own_in_place=not args.regroup_copy_own, one_call=not args.regroup_split_calls)
+                             own_in_place=not args.regroup_copy_own, one_call=not args.regroup_split_calls,
+                             slots=args.regroup_slots)
         except (RuntimeError, OSError, ValueError) as e:
             rg = {"error": f"{type(e).__name__}: {e}"}
         if rank == 0:
@@ -539,12 +544,17 @@ def cpu_baseline(host, shards, alive, seconds):
 
 
 def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8, exchange="c", own_in_place=True,
-                one_call=True):
+                one_call=True, slots=2):
     """Classify + regroup on its own batches of config `cfg` (C5 by default: mixed
     lengths, 64 shards). One step = one route launch of `per_step` batches, then ONE pack of all of
-    them by owner GPU (shard % G, sr_pack_many_by_owner) and ONE exchange: an all-to-all of the
-    split sizes (the step's single host round trip), of the packed lines and of the records (RCCL
-    over xGMI). Timed like the main region (barrier + synchronize, max over ranks)."""
+    them by owner GPU (shard % G) and ONE exchange: an all-to-all of the split sizes (the step's single
+    host round trip), of the packed lines and of the records (RCCL over xGMI). Timed like the main
+    region (barrier + synchronize, max over ranks).
+
+    slots = 2 (the C exchange): consecutive steps alternate between two router contexts, each with its
+    own stream, communicator, records and receive buffers, so step i + 1's route launch and split sizes
+    run while step i's scatter and exchange move its payload (the host's wait for step i + 1's sizes
+    overlaps step i's transfer); slots = 1: every step on one stream, strictly in sequence."""
     import torch
     import torch.distributed as dist
 
@@ -561,69 +571,95 @@ def regroup_leg(pkg, dev, local, world, rank, cfg, steps, per_step=8, exchange="
     d_in = torch.empty((nb, batch_bytes), dtype=torch.uint8, device=dev)
     for b, s in enumerate(host):
         d_in[b, : sizes[b]].copy_(torch.from_numpy(s.data))
-    stream = torch.cuda.Stream(device=dev)
-    router = pkg.Router(shards, batch_bytes, device=local)
-    router.set_stream(stream.cuda_stream)
-    d_rec = torch.empty((nb, max_lines), dtype=torch.int64, device=dev)
-    d_n = torch.zeros(nb, dtype=torch.int64, device=dev)
     base = d_in.data_ptr()
-    route_descs = [(base + b * batch_bytes, sizes[b], d_rec[b].data_ptr(), max_lines, None, d_n[b].data_ptr())
-                   for b in range(nb)]
-    pack_descs = [(base + b * batch_bytes, sizes[b], d_rec[b].data_ptr(), max_lines, d_n[b].data_ptr())
-                  for b in range(nb)]
+    if exchange != "c" or not own_in_place or not one_call:
+        slots = 1   # the developer A/B paths stay on one stream
 
-    comm, transport = None, "torch.distributed all_to_all_single (nccl)"
-    if exchange == "c":   # the C ABI's RCCL exchange (sr_exchange_sizes / sr_exchange_data)
-        err = ""
+    def open_comm():
+        err, comm = "", None
         try:
             comm = pkg.Comm.from_group(local)
         except (OSError, RuntimeError) as e:
             err = str(e)
         ok = torch.tensor([0.0 if comm is None else 1.0], device=dev)
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)   # every rank on the same transport
-        if ok.item() == 1.0:
-            transport = "C ABI sr_exchange_sizes + sr_exchange_data (RCCL)"
+        if ok.item() != 1.0 and comm is not None:
+            comm.close()
+            comm = None
+        return comm, err
+
+    class Slot:   # one router context: stream, records, communicator, regrouper
+        def __init__(self):
+            self.stream = torch.cuda.Stream(device=dev)
+            self.router = pkg.Router(shards, batch_bytes, device=local)
+            self.router.set_stream(self.stream.cuda_stream)
+            self.d_rec = torch.empty((nb, max_lines), dtype=torch.int64, device=dev)
+            self.d_n = torch.zeros(nb, dtype=torch.int64, device=dev)
+            self.route_descs = [(base + b * batch_bytes, sizes[b], self.d_rec[b].data_ptr(), max_lines, None,
+                                 self.d_n[b].data_ptr()) for b in range(nb)]
+            self.pack_descs = [(base + b * batch_bytes, sizes[b], self.d_rec[b].data_ptr(), max_lines,
+                                self.d_n[b].data_ptr()) for b in range(nb)]
+            self.comm = None
+
+    ss = [Slot() for _ in range(max(1, slots))]
+    transport = "torch.distributed all_to_all_single (nccl)"
+    if exchange == "c":   # the C ABI's RCCL exchange (sr_exchange_sizes / sr_exchange_data)
+        errs = []
+        for sl in ss:
+            sl.comm, err = open_comm()
+            errs.append(err)
+        if all(sl.comm is not None for sl in ss):
+            transport = "C ABI sr_regroup_launch (RCCL)" + (f", {len(ss)} communicators" if len(ss) > 1 else "")
         else:
-            if comm is not None:
-                comm.close()
-                comm = None
-            transport += f" (sr_comm_open failed on some rank{': ' + err if err else ''})"
-    with torch.cuda.stream(stream):
-        reg = rg_mod.LaunchRegrouper(pkg, router, sum(sizes), nb * max_lines, comm=comm, own_in_place=own_in_place,
-                                      one_call=one_call)
+            for sl in ss:
+                if sl.comm is not None:
+                    sl.comm.close()
+                    sl.comm = None
+            transport += f" (sr_comm_open failed on some rank{': ' + ' '.join(e for e in errs if e) if any(errs) else ''})"
+    for sl in ss:
+        with torch.cuda.stream(sl.stream):
+            sl.reg = rg_mod.LaunchRegrouper(pkg, sl.router, sum(sizes), nb * max_lines, comm=sl.comm,
+                                            own_in_place=own_in_place, one_call=one_call)
 
-        def step():
-            router.route_device_many(route_descs)
-            rb, rr, _ = reg(pack_descs)
-            sent = sum(c[1] for c in reg.last_sent) - reg.last_sent[rank][1]
-            return int(rr.numel()), int(rb.numel()), sent
+    def step(i):
+        sl = ss[i % len(ss)]
+        with torch.cuda.stream(sl.stream):
+            sl.router.route_device_many(sl.route_descs)
+            rb, rr, _ = sl.reg(sl.pack_descs)
+        sent = sum(c[1] for c in sl.reg.last_sent) - sl.reg.last_sent[rank][1]
+        return int(rr.numel()), int(rb.numel()), sent
 
-        for _ in range(2):
-            step()
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        acc = [0, 0, 0]
-        for _ in range(steps):
-            acc = [a + x for a, x in zip(acc, step())]
-        torch.cuda.synchronize()
-        dist.barrier()
-        wall = time.perf_counter() - t0
-    router.close()
-    if comm is not None:
-        comm.close()
+    for i in range(2 * len(ss)):
+        step(i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    acc = [0, 0, 0]
+    for i in range(steps):
+        acc = [a + x for a, x in zip(acc, step(i))]
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    for sl in ss:
+        sl.router.close()
+        if sl.comm is not None:
+            sl.comm.close()
     t = torch.tensor([wall], dtype=torch.float64, device=dev)
     tot = torch.tensor([sum(lines) * steps, acc[0], acc[1], acc[2]], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dist.all_reduce(tot, op=dist.ReduceOp.SUM)
     w = float(t[0])
+    comm = ss[0].comm
     return {"value": round(float(tot[0]) / w / 1e6, 3), "unit": "M metrics/s", "workload": desc,
             "steps_per_gpu": steps, "batches_per_step": nb, "ms_per_step": round(w * 1e3 / steps, 4),
+            "slots": len(ss),
             "lines_regrouped": int(tot[1]), "bytes_regrouped": int(tot[2]),
             "bytes_sent_to_other_gpus_per_s": round(float(tot[3]) / w / 1e9, 3), "exchange": transport,
             "note": (f"route launch of {nb} x 16 MiB batches + one pack by owner + one exchange (split sizes, "
                      f"packed lines, records) per step over {world} GPU(s); owner = shard % {world}; one host round "
                      f"trip per step for the split sizes; "
+                     + (f"steps alternate over {len(ss)} contexts and streams (step i + 1's route overlaps step i's "
+                        "scatter and exchange); " if len(ss) > 1 else "")
                      + (("sr_regroup_launch: " if one_call else "")
                         + "sr_pack_owner_sizes, then sr_pack_owner_scatter with the rank's own chunk written straight "
                         "into the receive buffers (no local copy)" if comm is not None and own_in_place
@@ -663,7 +699,7 @@ def verify_pack(pkg, th, host, M, max_lines, shards, alive):
 
 
 def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, dev, dead=False, reps=20,
-             alive=None, threads=2, host=None, knobs=()):
+             alive=None, threads=2, host=None, knobs=(), min_warmup_ms=60.0):
     """The router's device data path: one route launch over M batches (the
     batches of M data threads), then the per-downstream MTU packing of all of them in one
     sr_pack_packets_many (sorted records + packet descriptors, each batch from its own pending
@@ -722,10 +758,13 @@ def pack_leg(pkg, router, stream, d_in, sizes, lines, batch_bytes, shards, M, de
             getattr(th, attr).replay()
 
     def timed(threads, attr):
-        for th in threads:
-            for _ in range(3):
-                replay(th, attr)
-        torch.cuda.synchronize()
+        # the main leg's warm-up rule: back-to-back replays for at least min_warmup_ms (the clocks settle)
+        t_w = time.perf_counter()
+        while (time.perf_counter() - t_w) * 1e3 < min_warmup_ms:
+            for _ in range(8):
+                for th in threads:
+                    replay(th, attr)
+            torch.cuda.synchronize()
         a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(threads[0].st)
         for th in threads[1:]:

@@ -536,14 +536,7 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
             emit(lf, s_abs, len, len_ok, fmt_ok, h);
         }
     }
-    if (!(ABL & (KV_ALIVE | KV_DEFER1)) && p.mark_tiles && bd.probed_dead) {   // MARK_LDS: the dead shards this tile's probes visited
-        wg_barrier();
-        if ((uint32_t)tid < p.nwords) {
-            const uint32_t lo = sm.img[(kMarkRow0 + 2 * (uint32_t)tid) * 17 + 16];
-            const uint32_t hi = sm.img[(kMarkRow0 + 2 * (uint32_t)tid + 1) * 17 + 16];
-            p.tile_pd[(size_t)(bd.sbase + t) * p.nwords + tid] = ((uint64_t)hi << 32) | lo;
-        }
-    }
+    mark_tile_end<ABL>(p, sm.img, bd, t, tid);   // MARK_LDS: the dead shards this tile's probes visited
     if (tid == 0) arrive(p, blockIdx.x, ep0);
     prefetch_sink(pf);
     stamp<ABL>(p, tid, g, 9);

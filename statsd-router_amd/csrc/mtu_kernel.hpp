@@ -125,6 +125,11 @@ struct MtuLaunch {
     // in the batches' probed-dead bitmaps (fd_mark) before counting
     ProbeArgs probe;
     uint32_t fd_mark, nwords;
+    // group mode after a route launch with one dead shard: the route tiles' probed-dead slots ([tile][pd_words],
+    // tile = the batch's route tiles from b.tile0), ORed into each batch's bitmap by mtu_scan_kernel (no
+    // probe_defer_kernel); null: the bitmaps are complete
+    const uint64_t *tile_pd;
+    uint32_t pd_words, pad_pd;
     MtuBatchArg b[kMtuMaxBatches];
 };
 static_assert(sizeof(MtuLaunch) < 3584, "kernel argument size");
@@ -356,11 +361,28 @@ __global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuLaunch L) {
     const MtuParams p = mtu_view(L, blockIdx.x);
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t carry_s;
+    __shared__ unsigned long long pd_or[kReplayCheckWords];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t nk = p.nds + 1, ntiles = p.ntiles;
     const size_t total = (size_t)nk * ntiles;
+    // L.tile_pd (one dead shard, sr-main.c:106): the batch's probed-dead bitmap = the OR of its route tiles'
+    // slots (their probes' marks), issued first so that the loads overlap the scan
+    const bool or_slots = L.tile_pd && p.probed_dead && L.pd_words <= kReplayCheckWords;
+    const uint64_t *const slots = or_slots ? L.tile_pd + (size_t)L.b[blockIdx.x].tile0 * L.pd_words : nullptr;
+    uint64_t v0 = 0;
+    if (or_slots)
+        for (uint32_t t = tid; t < ntiles; t += 1024) v0 |= slots[(size_t)t * L.pd_words];
+    if (tid < (int)kReplayCheckWords) pd_or[tid] = 0ull;
     if (tid == 0) carry_s = 0;
     __syncthreads();
+    if (or_slots) {
+        if (v0) atomicOr(&pd_or[0], (unsigned long long)v0);
+        for (uint32_t w = 1; w < L.pd_words; ++w) {
+            uint64_t v = 0;
+            for (uint32_t t = tid; t < ntiles; t += 1024) v |= slots[(size_t)t * L.pd_words + w];
+            if (v) atomicOr(&pd_or[w], (unsigned long long)v);
+        }
+    }
     // 16 rows of 64 consecutive entries per wave and round (coalesced loads and stores, each row scanned
     // in registers): the route kernel's tile histograms (group mode) are 1024 tiles per 16 MiB batch, so
     // a batch of 16 shards scans 17 k entries
@@ -394,6 +416,8 @@ __global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuLaunch L) {
         __syncthreads();
     }
     const uint32_t n = mtu_lines(p);
+    if (or_slots && (uint32_t)tid < L.pd_words)   // (the scan's barriers ordered every OR before this)
+        const_cast<uint64_t *>(p.probed_dead)[tid] = pd_or[tid];
     for (uint32_t k = tid; k < nk; k += 1024) p.key_start[k] = ntiles ? p.tile_counts[(size_t)k * ntiles] : 0u;
     if (tid == 0) {
         p.key_start[nk] = n;
@@ -429,7 +453,8 @@ __global__ __launch_bounds__(1024) void mtu_scan_kernel(MtuLaunch L) {
     for (uint32_t s = tid; s < p.nds; s += 1024)
         if (p.key_start[s + 1] == p.key_start[s]) {
             const uint32_t x = p.fill_in ? min((uint32_t)p.fill_in[s], (uint32_t)kMtuCap) : 0u;
-            p.fill_out[s] = mtu_dropped(p, s) ? 0 : (uint16_t)x;
+            const bool dropped = or_slots ? ((pd_or[s >> 6] >> (s & 63)) & 1ull) != 0 : mtu_dropped(p, s);
+            p.fill_out[s] = dropped ? 0 : (uint16_t)x;
         }
 }
 

@@ -12,7 +12,7 @@
 // Lines routed to no shard (invalid length / format, all dead) are not packed: the GPU that
 // received them reports them (the WARN lines of sr-main.c:115,142,184 stay with the receiver).
 //
-// Three launches over tiles of kPackTile records (the tiles of all packed batches in sequence):
+// Three launches over tiles of 256 x CH records (the tiles of all packed batches in sequence):
 // per-tile counts, one workgroup scanning them, then the stable scatter (in-tile ranks recomputed
 // with ballots and DPP scans).
 #pragma once
@@ -22,12 +22,10 @@
 namespace srk {
 
 constexpr int kPackBlock = 256;
-#ifndef SR_PACK_CHUNKS
-#define SR_PACK_CHUNKS 2
-#endif
-constexpr int kPackChunks = SR_PACK_CHUNKS;                          // 256-record chunks per tile (long lines:
-                                                        // enough tiles to fill the chip)
-constexpr int kPackTile = kPackBlock * kPackChunks;     // records per tile
+// 256-record chunks per tile, chosen per pack (pack_chunks_for in sr_route.hip): two for short lines,
+// one when the lines are long, so that a launch of long lines has enough workgroups to balance the
+// scatter's copy (C5 one workgroup generation of 512-record tiles: 256-record tiles +3-4 %; C2 -2 %)
+constexpr int kPackMaxChunks = 2;
 constexpr int kMaxOwners = 64;
 
 // One routed batch of a pack (up to kPackMaxBatches per pack: a route launch's batches are packed
@@ -70,12 +68,13 @@ struct PackParams {
 // the batch of pack tile `tile` and the tile's first record in it (nb <= 32: a scan over SGPRs)
 // batch of a (wave-uniform) tile: lane j compares with batch j's first tile, one ballot (a loop over the
 // batches waited on one scalar load per batch)
+template <int CH>
 __device__ __forceinline__ const PackBatch &pack_batch_of(const PackParams &p, uint32_t tile, uint32_t &r0) {
     static_assert(kPackMaxBatches <= 64, "one lane per batch");
     const uint32_t lane = threadIdx.x & 63u;
     const bool past = lane >= 1 && lane < p.nb && tile >= p.b[lane < kPackMaxBatches ? lane : 0].tile0;
     const uint32_t k = (uint32_t)__popcll(__ballot(past));
-    r0 = (tile - p.b[k].tile0) * kPackTile;
+    r0 = (tile - p.b[k].tile0) * (uint32_t)(kPackBlock * CH);
     return p.b[k];
 }
 
@@ -95,26 +94,27 @@ __device__ __forceinline__ int pack_owner(const sr_record &r, uint32_t n_owners)
 #endif
 constexpr int kCountTiles = SR_COUNT_TILES;
 static_assert(offsetof(sr_record, length) == 4 && offsetof(sr_record, route) == 6, "{length, route} word");
+template <int CH>
 __global__ __launch_bounds__(kPackBlock) void pack_count_kernel(PackParams p) {
     __shared__ uint32_t s_lines[kCountTiles][kMaxOwners], s_bytes[kCountTiles][kMaxOwners];
     const int tid = threadIdx.x, lane = tid & 63;
     const uint32_t G = p.n_owners;
     const uint32_t t0 = blockIdx.x * kCountTiles;
     for (uint32_t o = tid; o < kCountTiles * G; o += kPackBlock) s_lines[o / G][o % G] = s_bytes[o / G][o % G] = 0;
-    uint32_t lr[kCountTiles][kPackChunks];
+    uint32_t lr[kCountTiles][CH];
     uint64_t nr[kCountTiles];
     uint32_t r0s[kCountTiles], cap[kCountTiles];
 #pragma unroll
     for (int tt = 0; tt < kCountTiles; ++tt) {
         const uint32_t t = min(t0 + tt, p.ntiles - 1);
         uint32_t r0;
-        const PackBatch &bt = pack_batch_of(p, t, r0);
+        const PackBatch &bt = pack_batch_of<CH>(p, t, r0);
         r0s[tt] = r0;
         cap[tt] = bt.max_records;
         nr[tt] = *bt.n_records;
         const uint32_t *w = reinterpret_cast<const uint32_t *>(bt.recs) + 1;
 #pragma unroll
-        for (int c = 0; c < kPackChunks; ++c)
+        for (int c = 0; c < CH; ++c)
             lr[tt][c] = w[2 * (size_t)min(r0 + c * kPackBlock + tid, bt.max_records - 1)];
     }
     __syncthreads();
@@ -123,7 +123,7 @@ __global__ __launch_bounds__(kPackBlock) void pack_count_kernel(PackParams p) {
         if (t0 + tt >= p.ntiles) break;
         const uint32_t n = (uint32_t)min(nr[tt], (uint64_t)cap[tt]);
 #pragma unroll
-        for (int c = 0; c < kPackChunks; ++c) {
+        for (int c = 0; c < CH; ++c) {
             const uint32_t i = r0s[tt] + c * kPackBlock + tid;
             int ow = -1;
             uint32_t len4 = 0;
@@ -223,6 +223,7 @@ __global__ __launch_bounds__(1024) void pack_scan_kernel(PackParams p) {
     }
 }
 
+template <int CH>
 __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) {
     __shared__ uint32_t s_run_l[kMaxOwners], s_run_b[kMaxOwners];   // running in-tile position per owner
     __shared__ uint32_t s_wl[4][kMaxOwners], s_wb[4][kMaxOwners];   // per-wave chunk totals
@@ -230,14 +231,14 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
     __shared__ uint32_t s_pre[kPackBlock];   // per wave: exclusive prefix of its lines' 16-byte pieces
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t r0;
-    const PackBatch &bt = pack_batch_of(p, blockIdx.x, r0);
+    const PackBatch &bt = pack_batch_of<CH>(p, blockIdx.x, r0);
     const uint32_t n = (uint32_t)min(*bt.n_records, (uint64_t)bt.max_records);
     const uint32_t G = p.n_owners;
     for (uint32_t o = tid; o < G; o += kPackBlock) s_run_l[o] = s_run_b[o] = 0;
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)bt.bytes, (short)0, (int)bt.nbytes, 0x00020000);
     __syncthreads();
-    for (int c = 0; c < kPackChunks; ++c) {
+    for (int c = 0; c < CH; ++c) {
         const uint32_t i = r0 + c * kPackBlock + tid;
         int ow = -1;
         sr_record r{0, 0, 0};

@@ -103,6 +103,9 @@ struct DeviceState {
     // fused deferral (route + pack launches, SR_KNOB_FUSE_DEFER, off by default): asked for by the caller, and whether
     // the last launch left its deferred probes to the packing's counting pass (mtu_count_kernel<true>)
     bool fuse_defer = false, last_fused = false;
+    // route + pack launches (sr_route_pack_many / _submit): the packing may OR the tiles' probed-dead slots
+    // (asked for by the caller), and whether the last launch left them to it (mtu_scan_kernel)
+    bool pack_ors_marks = false, last_marks_pending = false;
     uint32_t fd_mark = 0;
     const uint64_t *fd_dhash[kMaxBatches] = {};
 
@@ -476,6 +479,12 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
     // KV_DEAD1: exactly one dead shard (two picks end every probe)
     const bool dead1 = !(ABL & KV_ALIVE) && ds.dead == 1 && ds.nds >= 2;
     constexpr unsigned kK1 = (ABL & KV_ALIVE) ? ABL : (ABL | KV_DEAD1);
+    // A route + pack launch with one dead shard (KV_DEAD1 | KV_HIST1, nothing deferred): the packing's
+    // mtu_scan_kernel ORs the tiles' probed-dead slots into the bitmaps (pack_ors_marks); no
+    // probe_defer_kernel (7.2 us per C2 launch for that OR alone)
+    const bool slots_to_pack = ds.pack_ors_marks && dead1 && p.mark_tiles && p.hist && (ABL & KV_PICKS) != 0 &&
+                               !(ABL & KV_CHUNKS);
+    ds.last_marks_pending = slots_to_pack;
     if constexpr ((ABL & KV_CHUNKS) != 0) {
         static_assert(BLOCK == 256, "route_chunk_kernel: 256 lanes of 64 bytes per 16 KiB tile");
         // its probe stops after the first picks: with two or more dead shards it needs the deferral
@@ -508,7 +517,7 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
     // dead (KV_DEAD1: two picks end every probe in the kernel). (Counting them in the general picks-only
     // variant cost it 5 us per C2 launch in SGPR spills: profiles/r05/hist_one_dead_ab_r5h.jsonl.)
     ds.last_hist = p.hist && !(ABL & KV_CHUNKS) && ((ABL & KV_ALIVE) || ((ABL & KV_PICKS) && dead1));
-    if ((p.defer || p.mark) && !fused) {   // the probes past their first two picks and the OR of the tiles' probed-dead
+    if ((p.defer || p.mark) && !fused && !slots_to_pack) {   // the probes past their first two picks and the OR of the tiles' probed-dead
                                // slots (probe_defer_kernel), grid y = batch
         // blocks past a batch's record count return at once; the rest loop over chunks of 4 waves
         const uint32_t bx = p.defer ? (max_recs + 4u * kDeferChunk - 1u) / (4u * kDeferChunk) : 1u;

@@ -779,6 +779,13 @@ __device__ __forceinline__ uint32_t dead1_probe(uint64_t h, const RouteParams &p
     return j2 == j ? n - 1 : j2;
 }
 
+// The end of a tile's MARK_LDS (the dead shards its probes visited, sr-main.c:106): its words go to its
+// slot (plain stores, nothing waits), ORed per batch after the launch by probe_defer_kernel or, in a
+// route + pack launch with one dead shard, by the packing's mtu_scan_kernel.
+template <unsigned ABL>
+__device__ __forceinline__ void mark_tile_end(const RouteParams &p, const uint32_t *img, const BatchDesc &bd, uint32_t t,
+                                              int tid);
+
 // ---------------------------------------------------------------------------------------
 // The route kernel
 // ---------------------------------------------------------------------------------------
@@ -1929,14 +1936,7 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     uint32_t c_in;
     tile_load<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
     tile_lines<BLOCK, ABL>(p, sm, in, ep0, g, nlm, clm, c_in);
-    if (!(ABL & (KV_ALIVE | KV_DEFER1)) && p.mark_tiles && p.b[bi].probed_dead) {   // MARK_LDS: the dead shards this tile's probes visited
-        wg_barrier();
-        if ((uint32_t)tid < p.nwords) {   // the tile's slot, ORed by probe_defer_kernel (no atomics)
-            const uint32_t lo = sm.img[(kMarkRow0 + 2 * (uint32_t)tid) * 17 + 16];
-            const uint32_t hi = sm.img[(kMarkRow0 + 2 * (uint32_t)tid + 1) * 17 + 16];
-            p.tile_pd[(size_t)(p.b[bi].sbase + t) * p.nwords + tid] = ((uint64_t)hi << 32) | lo;
-        }
-    }
+    mark_tile_end<ABL>(p, sm.img, p.b[bi], t, tid);   // MARK_LDS: the dead shards this tile's probes visited
     if (kCountsHist<ABL> && p.hist) {   // the tile's key histogram for the packing (sr_route_pack_many)
         wg_barrier();
         const BatchDesc &bd = p.b[bi];
@@ -1945,6 +1945,18 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     }
     if (tid == 0) arrive(p, blockIdx.x, ep0);
     stamp<ABL>(p, tid, g, 9);
+}
+
+template <unsigned ABL>
+__device__ __forceinline__ void mark_tile_end(const RouteParams &p, const uint32_t *img, const BatchDesc &bd, uint32_t t,
+                                              int tid) {
+    if ((ABL & (KV_ALIVE | KV_DEFER1)) || !p.mark_tiles || !bd.probed_dead) return;
+    wg_barrier();
+    if ((uint32_t)tid < p.nwords) {   // the tile's slot (no atomics)
+        const uint32_t lo = img[(kMarkRow0 + 2 * (uint32_t)tid) * 17 + 16];
+        const uint32_t hi = img[(kMarkRow0 + 2 * (uint32_t)tid + 1) * 17 + 16];
+        p.tile_pd[(size_t)(bd.sbase + t) * p.nwords + tid] = ((uint64_t)hi << 32) | lo;
+    }
 }
 
 // After a route launch with dead shards. MARK_LDS: block 0 of each batch ORs the tiles' probed-dead

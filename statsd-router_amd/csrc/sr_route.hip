@@ -334,6 +334,18 @@ int sr_route_device_many(sr_ctx *c, const sr_batch *batches, size_t count) {
     return 0;
 }
 
+// The owner pack's tile: 256 records per chunk, two chunks per tile when the pack's lines are short,
+// one when they are long (more than 192 bytes per record slot on average: C5's mixed lines, C3, C4).
+// Every call with the same batches picks the same (sr_pack_owner_sizes and _scatter share the tiles).
+static int pack_chunks_for(const PackBatch *in, uint32_t nb) {
+    uint64_t bytes = 0, recs = 0;
+    for (uint32_t j = 0; j < nb; ++j) {
+        bytes += in[j].nbytes;
+        recs += in[j].max_records;
+    }
+    return bytes > 192ull * (recs ? recs : 1) ? 1 : kPackMaxChunks;
+}
+
 // The owner pack: kPackSizes = count + scan (the split sizes into d_owner_counts), kPackScatter =
 // the lines and records (owner `own` into own_bytes / own_recs when own >= 0)
 enum : int { kPackSizes = 1, kPackScatter = 2 };
@@ -342,11 +354,13 @@ static int pack_launch(sr_ctx *c, const PackBatch *in, uint32_t nb, uint32_t n_o
                        int own = -1, uint8_t *own_bytes = nullptr, sr_record *own_recs = nullptr) {
     PackParams p;
     memset(&p, 0, sizeof(p));
+    const int ch = pack_chunks_for(in, nb);
+    const uint32_t tile = (uint32_t)(kPackBlock * ch);
     uint32_t ntiles = 0;
     for (uint32_t j = 0; j < nb; ++j) {
         p.b[j] = in[j];
         p.b[j].tile0 = ntiles;
-        ntiles += (in[j].max_records + kPackTile - 1) / kPackTile;
+        ntiles += (in[j].max_records + tile - 1) / tile;
     }
     p.nb = nb ? nb : 1;
     p.n_owners = n_owners;
@@ -372,7 +386,9 @@ static int pack_launch(sr_ctx *c, const PackBatch *in, uint32_t nb, uint32_t n_o
     p.own_bytes = own_bytes;
     p.own_recs = own_recs;
     if ((phases & kPackSizes) && ntiles) {
-        hipLaunchKernelGGL(pack_count_kernel, dim3((ntiles + kCountTiles - 1) / kCountTiles), dim3(kPackBlock), 0, c->stream, p);
+        const dim3 grid((ntiles + kCountTiles - 1) / kCountTiles);
+        if (ch == 1) hipLaunchKernelGGL(pack_count_kernel<1>, grid, dim3(kPackBlock), 0, c->stream, p);
+        else hipLaunchKernelGGL(pack_count_kernel<kPackMaxChunks>, grid, dim3(kPackBlock), 0, c->stream, p);
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
     if (phases & kPackSizes) {
@@ -380,7 +396,8 @@ static int pack_launch(sr_ctx *c, const PackBatch *in, uint32_t nb, uint32_t n_o
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
     if ((phases & kPackScatter) && ntiles) {
-        hipLaunchKernelGGL(pack_scatter_kernel, dim3(ntiles), dim3(kPackBlock), 0, c->stream, p);
+        if (ch == 1) hipLaunchKernelGGL(pack_scatter_kernel<1>, dim3(ntiles), dim3(kPackBlock), 0, c->stream, p);
+        else hipLaunchKernelGGL(pack_scatter_kernel<kPackMaxChunks>, dim3(ntiles), dim3(kPackBlock), 0, c->stream, p);
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
     return 0;
@@ -540,7 +557,7 @@ extern "C" size_t sr_mtu_stamps(uint64_t *dst, size_t max_chunks) {
 // context's last route launch (RouteParams::hist); route_bytes: each batch's bytes in that launch
 // (its tiles: ceil(bytes / 16 KiB), numbered in batch order as launch_route numbers them)
 static int pack_many_impl(sr_ctx *c, const sr_pack_batch *batches, size_t count, uint32_t *hist,
-                          const size_t *route_bytes, bool fused = false) {
+                          const size_t *route_bytes, bool fused = false, const uint64_t *tile_pd = nullptr) {
     if (!c || !batches || count == 0 || count > (size_t)kMtuMaxBatches) return -EINVAL;
     const uint32_t nds = c->ds.nds;
     if (nds > SR_MAX_PACK_DOWNSTREAMS) return -EINVAL;
@@ -605,6 +622,9 @@ static int pack_many_impl(sr_ctx *c, const sr_pack_batch *batches, size_t count,
     L.table = c->d_mtu_table;
     L.nx = reinterpret_cast<uint8_t *>(c->d_mtu_table + (((size_t)c->mtu_chunks * kMtuX + 1) & ~(size_t)1));
     L.plen = reinterpret_cast<uint16_t *>(c->d_mtu_gp);
+    // group mode after a one-dead-shard launch: mtu_scan ORs the route tiles' probed-dead slots
+    L.tile_pd = hist ? tile_pd : nullptr;
+    L.pd_words = c->ds.nwords;
     L.gp0 = c->d_mtu_gp + (size_t)c->mtu_chunks * kMtuChunk / 2;
     if (fused) {   // the route launch's deferred probes, run by the counting pass
         if (hist) return -EIO;
@@ -717,12 +737,19 @@ static int route_pack_impl(sr_ctx *c, const sr_batch *route, const sr_pack_batch
     p.hist = want ? ds.d_hist : nullptr;
     ds.last_hist = false;
     ds.fuse_defer = c->fuse_defer && !want;
+    ds.pack_ors_marks = want;
+    ds.last_marks_pending = false;
     int rc = launch_variant(ds, p, c->stream);
     ds.fuse_defer = false;
+    ds.pack_ors_marks = false;
     if (rc) return rc;
     const bool fused = ds.last_fused;
     ds.last_fused = false;
-    return pack_many_impl(c, pack, count, ds.last_hist ? ds.d_hist : nullptr, bytes, fused);
+    const bool marks = ds.last_marks_pending;   // the tiles' probed-dead slots, for mtu_scan to OR
+    ds.last_marks_pending = false;
+    if (marks && !ds.last_hist) return -EIO;   // (never: such launches ran the KV_HIST1 kernel)
+    return pack_many_impl(c, pack, count, ds.last_hist ? ds.d_hist : nullptr, bytes, fused,
+                          marks ? ds.d_tile_pd : nullptr);
 }
 
 int sr_route_pack_many(sr_ctx *c, const sr_batch *route, const sr_pack_batch *pack, size_t count) {
