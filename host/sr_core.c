@@ -258,14 +258,15 @@ static void trace_line(sr_core *c, const char *line, int len, uint64_t h, uint32
 
 /* TRACE: every message of udp_read_cb for the batch in slot `slot`, in input order: per datagram
  * "got packet" (sr-main.c:174), then per line its WARN (:142,184) or its find_downstream lines. */
-static void trace_batch(sr_core *c, int slot, const uint8_t *framed, size_t nbytes) {
+static int trace_batch(sr_core *c, int slot, const uint8_t *framed, size_t nbytes) {
     const sr_record *rec;
     const uint64_t *hs;
     size_t n = 0, i = 0, d0 = 0;
     int rc = sr_route_pack_trace(c->ctx, slot, &rec, &hs, &n);
     if (rc) {
         core_log(c, SR_ERROR, "%s: sr_route_pack_trace() failed %s", "udp_read_cb", strerror(-rc));
-        return;
+        c->dg_n[slot] = 0;
+        return rc;
     }
     const size_t nd = c->dg_n[slot];
     for (size_t g = 0; g <= nd; g++) {   /* the datagrams, then whatever no boundary covers */
@@ -281,6 +282,7 @@ static void trace_batch(sr_core *c, int slot, const uint8_t *framed, size_t nbyt
         d0 = end;
     }
     c->dg_n[slot] = 0;
+    return 0;
 }
 
 /* The host's half of a batch (udp_read_cb's per-line side effects, sr-main.c:175-189, for a whole
@@ -288,9 +290,9 @@ static void trace_batch(sr_core *c, int slot, const uint8_t *framed, size_t nbyt
 static void complete(sr_core *c, int slot, const uint8_t *framed, size_t nbytes, const sr_pack_result *r) {
     memcpy(c->probed, r->probed_dead, c->nwords * sizeof(uint64_t));
     drop_probed(c);
-    if (c->trace)
-        trace_batch(c, slot, framed, nbytes);
-    else if (c->log_level <= SR_WARN)
+    /* without the TRACE inputs (the slot was not traced) the WARN lines still come, from the sorted
+     * records' unrouted tail, in input order */
+    if ((!c->trace || trace_batch(c, slot, framed, nbytes) != 0) && c->log_level <= SR_WARN)
         for (size_t i = r->n_valid; i < r->n_records; i++) warn_line(c, framed, &r->sorted[i]);
     for (size_t q = 0; q < r->n_packets; q++) {
         const sr_packet *p = &r->packets[q];

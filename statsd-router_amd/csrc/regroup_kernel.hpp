@@ -223,12 +223,22 @@ __global__ __launch_bounds__(1024) void pack_scan_kernel(PackParams p) {
     }
 }
 
+__device__ __forceinline__ void pack_wave_sync() {   // LDS hand-off between the lanes of one wave
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// The scatter's copy works in windows of kPackWin 16-byte pieces per wave (16 per lane).
+constexpr uint32_t kPackWin = 1024;
+
 template <int CH>
 __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) {
     __shared__ uint32_t s_run_l[kMaxOwners], s_run_b[kMaxOwners];   // running in-tile position per owner
     __shared__ uint32_t s_wl[4][kMaxOwners], s_wb[4][kMaxOwners];   // per-wave chunk totals
-    __shared__ uint32_t s_src[kPackBlock], s_dst[kPackBlock], s_len[kPackBlock];
-    __shared__ uint32_t s_pre[kPackBlock];   // per wave: exclusive prefix of its lines' 16-byte pieces
+    // per wave, its owned lines in order (compacted): {source offset, destination, length | own << 31,
+    // first piece}; and per window a bitmap of the pieces where a line starts, with per-dword prefix counts
+    __shared__ uint4 s_info[4][64];
+    __shared__ uint32_t s_bm[4][kPackWin / 32], s_bp[4][kPackWin / 32];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     uint32_t r0;
     const PackBatch &bt = pack_batch_of<CH>(p, blockIdx.x, r0);
@@ -237,6 +247,7 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
     for (uint32_t o = tid; o < G; o += kPackBlock) s_run_l[o] = s_run_b[o] = 0;
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)bt.bytes, (short)0, (int)bt.nbytes, 0x00020000);
+    const uint64_t lt = (1ull << lane) - 1ull;
     __syncthreads();
     for (int c = 0; c < CH; ++c) {
         const uint32_t i = r0 + c * kPackBlock + tid;
@@ -257,7 +268,7 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
             const uint32_t v = ow == (int)o ? len4 : 0u;
             const uint32_t incl = wave_incl_add32(v);
             if (ow == (int)o) {
-                my_l = __popcll(m & ((1ull << lane) - 1ull));
+                my_l = __popcll(m & lt);
                 my_b = incl - v;
             }
             if (lane == 63) {
@@ -285,13 +296,14 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
                 p.out_recs[p.owner_start[2 * ow] + tb.x + pl + my_l] = o;
             }
         }
-        s_src[tid] = r.offset;
-        s_dst[tid] = dst;
-        s_len[tid] = ow >= 0 ? r.length | (ow == p.own ? 0x80000000u : 0u) : 0u;
+        // the wave's owned lines compacted (k = rank among them), with their first piece
         const uint32_t npc = ow >= 0 ? ((uint32_t)r.length + 15u) >> 4 : 0u;
+        const uint64_t owned = __ballot(npc != 0);
         const uint32_t pinc = wave_incl_add32(npc);
-        s_pre[tid] = pinc - npc;
+        const uint32_t pre = pinc - npc;
         const uint32_t T = __builtin_amdgcn_readlane(pinc, 63);
+        if (npc) s_info[wave][__popcll(owned & lt)] =
+            make_uint4(r.offset, dst, r.length | (ow == p.own ? 0x80000000u : 0u), pre);
         __syncthreads();
         if (tid < (int)G) {
             uint32_t al = 0, ab = 0;
@@ -304,58 +316,77 @@ __global__ __launch_bounds__(kPackBlock) void pack_scatter_kernel(PackParams p) 
         }
         constexpr int kCopyBatch = SR_PACK_COPY_BATCH;
         const uint64_t own_cap = p.own >= 0 ? p.owner_counts[2 * p.own + 1] : 0ull;
-        // copy the wave's 64 lines as one list of 16-byte pieces (a line of L bytes has ceil(L / 16)):
-        // lane i takes piece i, i + 64, ... and finds its line by a binary search over the wave's piece
-        // prefix, so every lane moves 16 bytes per pass whatever the mix of lengths (lanes per line left
-        // most lanes idle on mixed lines). Per piece: one dwordx4 buffer load at the source's byte offset
-        // (unaligned buffer access; byte loads for the one piece that crosses the batch's end), a dwordx4
-        // store where the padded line covers it, zero fill after the line; the loads of kCopyBatch passes
-        // issued before their stores
-        const uint32_t *pre = s_pre + wave * 64;
-        for (uint32_t s0 = lane; s0 < T; s0 += 64u * kCopyBatch) {
-            uint4 v[kCopyBatch];
-            uint32_t kq[kCopyBatch];   // line (6 bits) | byte within it << 6; ~0 past the end
+        // Copy the wave's lines as one list of 16-byte pieces (a line of L bytes has ceil(L / 16)), every
+        // lane moving 16 bytes per pass whatever the mix of lengths. Per window of kPackWin pieces: a bitmap
+        // of the pieces where an owned line starts, and its per-dword prefix counts; the line of piece sp
+        // is then (lines started before the window) + (starts at or before sp in it) - 1: two independent
+        // LDS reads, then the line's record (a binary search over the wave's piece prefix took six
+        // dependent LDS reads per piece). Per piece one dwordx4 buffer load at the source's byte offset
+        // (unaligned buffer access; byte loads for the one piece that crosses the batch's end), then a
+        // dwordx4 store, the line's last piece zero-filled to its 4-byte padding; the loads of kCopyBatch
+        // passes issued before their stores
+        uint32_t *const bm = s_bm[wave], *const bp = s_bp[wave];
+        const uint4 *const info = s_info[wave];
+        for (uint32_t w0 = 0; w0 < T; w0 += kPackWin) {
+            if (lane < (int)(kPackWin / 32)) bm[lane] = 0u;
+            pack_wave_sync();
+            if (npc && pre >= w0 && pre < w0 + kPackWin) atomicOr(&bm[(pre - w0) >> 5], 1u << ((pre - w0) & 31u));
+            const uint32_t kb = (uint32_t)__popcll(__ballot(npc != 0 && pre < w0));   // lines started before w0
+            pack_wave_sync();
+            const uint32_t cnt = lane < (int)(kPackWin / 32) ? (uint32_t)__popc(bm[lane]) : 0u;
+            const uint32_t cin = wave_incl_add32(cnt);
+            if (lane < (int)(kPackWin / 32)) bp[lane] = cin - cnt + kb;
+            pack_wave_sync();
+            const uint32_t wn = min(T - w0, kPackWin);
+            for (uint32_t l0 = lane; l0 < wn; l0 += 64u * kCopyBatch) {
+                uint4 v[kCopyBatch];
+                uint32_t kq[kCopyBatch];   // line (6 bits) | byte within it << 6; ~0 past the window
 #pragma unroll
-            for (int i = 0; i < kCopyBatch; ++i) {
-                const uint32_t sp = s0 + 64u * i;
-                v[i] = make_uint4(0, 0, 0, 0);
-                kq[i] = ~0u;
-                if (sp < T) {
-                    uint32_t j = 0;
+                for (int u = 0; u < kCopyBatch; ++u) {
+                    const uint32_t lc = l0 + 64u * u;
+                    v[u] = make_uint4(0, 0, 0, 0);
+                    kq[u] = ~0u;
+                    if (lc < wn) {
+                        const uint32_t d = lc >> 5;
+                        const uint32_t k = bp[d] + (uint32_t)__popc(bm[d] & (0xFFFFFFFFu >> (31u - (lc & 31u)))) - 1u;
+                        const uint4 in = info[k];
+                        const uint32_t q = (w0 + lc - in.w) << 4;
+                        kq[u] = k | (q << 6);
+                        v[u] = load16(rsrc, in.x + q, bt.nbytes);
+                    }
+                }
 #pragma unroll
-                    for (uint32_t st = 32; st; st >>= 1) j += pre[j + st] <= sp ? st : 0u;
-                    const uint32_t q = (sp - pre[j]) << 4;
-                    kq[i] = j | (q << 6);
-                    // the piece that straddles the batch's end by bytes (a 16-byte buffer load's range
-                    // check is not byte-exact: bytes before the end could read as zero)
-                    v[i] = load16(rsrc, s_src[wave * 64 + j] + q, bt.nbytes);
+                for (int u = 0; u < kCopyBatch; ++u) {
+                    if (kq[u] == ~0u) break;
+                    const uint32_t q = kq[u] >> 6;
+                    const uint4 in = info[kq[u] & 63u];
+                    const bool mine = (in.z >> 31) != 0;
+                    const uint32_t L = in.z & 0x7FFFFFFFu, d = in.y;
+                    uint8_t *const out = mine ? p.own_bytes : p.out_bytes;
+                    const uint64_t cap = mine ? own_cap : p.out_cap;
+                    uint8_t *o = out + d + q;
+                    if (q + 16u <= L && (uint64_t)d + q + 16u <= cap) {   // a whole piece of the line
+                        *(uint4 *)o = v[u];
+                    } else {   // the line's last piece: zero fill up to its 4-byte padding
+                        const uint32_t L4 = pack_len4(L);
+                        uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+                        for (int jj = 0; jj < 4; ++jj) {
+                            const uint32_t qj = q + 4u * jj;
+                            if (qj >= L) w[jj] = 0;
+                            else if (qj + 4u > L) w[jj] &= (1u << (8u * (L - qj))) - 1u;
+                        }
+                        if (q + 16u <= L4 && (uint64_t)d + q + 16u <= cap) {
+                            *(uint4 *)o = make_uint4(w[0], w[1], w[2], w[3]);
+                        } else {
+#pragma unroll
+                            for (int jj = 0; jj < 4; ++jj)
+                                if (q + 4u * jj < L4 && (uint64_t)d + q + 4u * jj + 4u <= cap) ((uint32_t *)o)[jj] = w[jj];
+                        }
+                    }
                 }
             }
-#pragma unroll
-            for (int i = 0; i < kCopyBatch; ++i) {
-                if (kq[i] == ~0u) break;
-                const uint32_t k = wave * 64 + (kq[i] & 63u), q = kq[i] >> 6;
-                const uint32_t Lf = s_len[k];
-                const bool mine = (Lf >> 31) != 0;
-                const uint32_t L = Lf & 0x7FFFFFFFu, L4 = pack_len4(L), d = s_dst[k];
-                uint8_t *const out = mine ? p.own_bytes : p.out_bytes;
-                const uint64_t cap = mine ? own_cap : p.out_cap;
-                uint32_t w[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
-#pragma unroll
-                for (int jj = 0; jj < 4; ++jj) {   // zero fill after the line
-                    const uint32_t qj = q + 4u * jj;
-                    if (qj >= L) w[jj] = 0;
-                    else if (qj + 4u > L) w[jj] &= (1u << (8u * (L - qj))) - 1u;
-                }
-                uint8_t *o = out + d + q;
-                if (q + 16u <= L4 && (uint64_t)d + q + 16u <= cap) {
-                    *(uint4 *)o = make_uint4(w[0], w[1], w[2], w[3]);
-                } else {
-#pragma unroll
-                    for (int jj = 0; jj < 4; ++jj)
-                        if (q + 4u * jj < L4 && (uint64_t)d + q + 4u * jj + 4u <= cap) ((uint32_t *)o)[jj] = w[jj];
-                }
-            }
+            pack_wave_sync();   // the window's bitmap is read to the end before the next is built
         }
         __syncthreads();
     }

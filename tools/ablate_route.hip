@@ -142,12 +142,25 @@ int main(int argc, char **argv) {
     std::vector<Row> rows;
     const int reps = 8;
     const bool quick = argc > 2 && std::string(argv[2]) == "quick";   // the parts of a 32-batch launch only
+    // "alive": the shipped every-shard-alive kernel (KV_UNIFORM | KV_ALIVE, C2's) with its phases switched off
+    // one at a time, 32-batch launches (per-phase VALU with tools/pmc_ablate.sh)
+    const bool alive = argc > 2 && std::string(argv[2]) == "alive";
     for (int round = 0; round < 3; ++round) {
         int i = 0;
         auto put = [&](const char *name, float us) {
             if (round == 0) rows.push_back(Row{name, {0, 0, 0}});
             rows[i++].us[round] = us;
         };
+        if (alive) {
+            put("alive", time_variant<256, KV_ALIVE>(c, 1, reps, 32));
+            put("alive_no_hash", time_variant<256, KV_ALIVE | ABL_NO_HASH>(c, 1, reps, 32));
+            put("alive_no_lines", time_variant<256, KV_ALIVE | ABL_NO_LINES>(c, 1, reps, 32));
+            put("alive_no_lines_no_prologue", time_variant<256, KV_ALIVE | ABL_NO_LINES | ABL_NO_PROLOGUE>(c, 1, reps, 32));
+            put("alive_load_only", time_variant<256, KV_ALIVE | ABL_LOAD_ONLY | ABL_NO_LOOKBACK | ABL_NO_PROLOGUE>(c, 1, reps, 32));
+            put("alive_fake_base", time_variant<256, KV_ALIVE | ABL_FAKE_BASE>(c, 1, reps, 32));
+            put("read_kernel_s1", time_variant<256, 0xFFFFu>(c, 1, reps));
+            continue;
+        }
         if (quick) {
             put("m32", time_variant<256, ABL_NONE>(c, 1, reps, 32));
             put("m32_fake_base", time_variant<256, ABL_FAKE_BASE>(c, 1, reps, 32));
@@ -188,7 +201,7 @@ int main(int argc, char **argv) {
         put("read_kernel_s4", time_variant<256, 0xFFFFu>(c, 4, reps));
     }
     // correctness: each product-shaped variant's line count on batch 0
-    if (!quick) {
+    if (!quick && !alive) {
         uint64_t n = 0;
         const RouteParams p = c.ds[0].params(c.batches[0], c.sizes[0], c.d_out[0][0], c.max_lines, nullptr, c.d_n);
         launch_route<1024, ABL_NONE>(c.ds[0], p, c.s[0]);
@@ -200,7 +213,7 @@ int main(int argc, char **argv) {
         CK(hipStreamSynchronize(c.s[0]));
         fprintf(stderr, "b512 lines %llu expected %zu\n", (unsigned long long)n, lines[0]);
     }
-    if (!quick) {   // multi-batch launch: every batch's line count
+    if (!quick && !alive) {   // multi-batch launch: every batch's line count
         std::vector<uint64_t> n(16);
         RouteParams p = c.ds[0].params();
         for (int k = 0; k < 16; ++k)
