@@ -521,8 +521,10 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
                                // slots (probe_defer_kernel), grid y = batch
         // blocks past a batch's record count return at once; the rest loop over chunks of 4 waves
         const uint32_t bx = p.defer ? (max_recs + 4u * kDeferChunk - 1u) / (4u * kDeferChunk) : 1u;
-        hipLaunchKernelGGL(probe_defer_kernel, dim3(bx ? (bx < 128u ? bx : 128u) : 1u, p.nb), dim3(256), 0, stream,
-                           p);
+        const dim3 grid(bx ? (bx < 128u ? bx : 128u) : 1u, p.nb);
+        if (ds.dead <= 4) hipLaunchKernelGGL(probe_defer_kernel<4>, grid, dim3(256), 0, stream, p);
+        else if (ds.dead <= 8) hipLaunchKernelGGL(probe_defer_kernel<8>, grid, dim3(256), 0, stream, p);
+        else hipLaunchKernelGGL(probe_defer_kernel<kOverlay>, grid, dim3(256), 0, stream, p);
         if (hipGetLastError() != hipSuccess) return -EIO;
     }
     if (ds.wide()) {

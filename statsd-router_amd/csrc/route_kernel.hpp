@@ -655,7 +655,9 @@ struct ProbeArgs {
     const Magic *magic;
 };
 
-template <bool MARK = false, class P = RouteParams>
+// OV: entries of the register overlay (at least the dead shards of the snapshot, or up to kOverlay: a probe
+// that would need more returns kRoutePending for probe_wide_kernel); fewer entries, fewer registers
+template <bool MARK = false, class P = RouteParams, int OV = kOverlay>
 __device__ uint32_t probe_shard(uint64_t h, const P &p, uint64_t *mark = nullptr,
                                 const uint32_t *pad_img = nullptr, unsigned long long *mark_wg = nullptr,
                                 bool defer = false, uint32_t *mark_lds = nullptr) {
@@ -698,15 +700,16 @@ __device__ uint32_t probe_shard(uint64_t h, const P &p, uint64_t *mark = nullptr
         h = (h * 7 + 5) / 3;                                                              // :113
     }
     if (defer && i > 0) return kRouteDefer;
-    uint32_t ov[kOverlay];
+    static_assert(OV >= 2 && OV <= kOverlay, "overlay entries");
+    uint32_t ov[OV];
     int nov = (o0 != 0xFFFFFFFFu) + (o1 != 0xFFFFFFFFu);
 #pragma unroll
-    for (int e = 0; e < kOverlay; ++e) ov[e] = e == 0 ? o0 : (e == 1 ? o1 : 0xFFFFFFFFu);
+    for (int e = 0; e < OV; ++e) ov[e] = e == 0 ? o0 : (e == 1 ? o1 : 0xFFFFFFFFu);
     for (; i > 0; --i) {
         const uint32_t j = mod_magic(h, magic_i(i), i);              // :98
         uint32_t k = j;                                              // :99
 #pragma unroll
-        for (int e = 0; e < kOverlay; ++e)
+        for (int e = 0; e < OV; ++e)
             if ((ov[e] >> 16) == j) k = ov[e] & 0xFFFFu;
         if (alive_k(k)) return k;                                    // :101-104
         if (MARK) note_dead_wg(mark, mark_wg, k);                    // :106
@@ -714,11 +717,11 @@ __device__ uint32_t probe_shard(uint64_t h, const P &p, uint64_t *mark = nullptr
         if (j != i - 1) {                                            // :108-111
             uint32_t v = i - 1;
 #pragma unroll
-            for (int e = 0; e < kOverlay; ++e)
+            for (int e = 0; e < OV; ++e)
                 if ((ov[e] >> 16) == i - 1) v = ov[e] & 0xFFFFu;
-            if (nov == kOverlay) return kRoutePending;
+            if (nov == OV) return kRoutePending;
 #pragma unroll
-            for (int e = 0; e < kOverlay; ++e)
+            for (int e = 0; e < OV; ++e)
                 if (e == nov) ov[e] = (j << 16) | v;
             ++nov;
         }
@@ -1990,6 +1993,9 @@ __device__ __forceinline__ void load_probe_pads(const RouteParams &p, uint32_t *
 
 constexpr uint32_t kDeferChunk = 256;   // records per wave and chunk (4 per lane)
 constexpr uint32_t kDeferOrBlocks = 16; // blocks per batch that OR the tiles' probed-dead slots (MARK_LDS)
+// OV: probe_shard's overlay entries, at least the snapshot's dead shards (launch_route picks 4, 8 or 16:
+// two of four shards dead need two entries, not sixteen registers' worth of unrolled overlay)
+template <int OV>
 __global__ __launch_bounds__(256) void probe_defer_kernel(RouteParams p) {
     __shared__ uint32_t pads[kProbePads];
     __shared__ uint32_t list[4][kDeferChunk];
@@ -2050,10 +2056,22 @@ __global__ __launch_bounds__(256) void probe_defer_kernel(RouteParams p) {
             cnt += __popcll(m);
         }
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t i = lane; i < cnt; i += 64u) {
-            const uint32_t x = list[w][i];
-            const uint64_t h = bd.dhash[x];
-            const uint32_t route = mark ? probe_shard<true>(h, p, mark, pads, wg) : probe_shard(h, p, nullptr, pads);
+        // every hash of the chunk's list requested before the first probe (at most four per lane)
+        uint32_t xs[kDeferChunk / 64];
+        uint64_t hs[kDeferChunk / 64];
+#pragma unroll
+        for (uint32_t it = 0; it < kDeferChunk / 64; ++it) {
+            const uint32_t i = lane + 64u * it;
+            xs[it] = i < cnt ? list[w][i] : 0u;
+            hs[it] = i < cnt ? bd.dhash[xs[it]] : 0ull;
+        }
+#pragma unroll
+        for (uint32_t it = 0; it < kDeferChunk / 64; ++it) {
+            if (lane + 64u * it >= cnt) break;
+            const uint32_t x = xs[it];
+            const uint64_t h = hs[it];
+            const uint32_t route = mark ? probe_shard<true, RouteParams, OV>(h, p, mark, pads, wg)
+                                        : probe_shard<false, RouteParams, OV>(h, p, nullptr, pads);
             if (route == kRoutePending) {   // more than kOverlay dead probes: probe_wide_kernel
                 const uint32_t slot = atomicAdd(&p.ctl->pending, 1u);
                 if (slot < p.pending_cap) p.pending[slot] = PendingLine{x, bi, h};

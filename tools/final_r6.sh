@@ -37,7 +37,8 @@ for st in $steps; do
     for c in c5 c2 c3; do b regroup_${c}_slots2 --config $c --steps 20 --no-cpu --no-e2e --no-pack --regroup on --regroup-config $c --regroup-steps 24; done
     b regroup_c5_slots1 --config c5 --steps 20 --no-cpu --no-e2e --no-pack --regroup on --regroup-config c5 --regroup-steps 24 --regroup-slots 1 ;;
   prof)
-    for job in "c2|--config c2" "c5|--config c5" "c5_regroup|--config c5 --steps 20 --no-pack --regroup on --regroup-steps 24"; do
+    for job in "c2|--config c2" "c5|--config c5" "c3_dead|--config c3 --dead 0.25" \
+               "c5_regroup|--config c5 --steps 20 --no-pack --regroup on --regroup-steps 24"; do
       name=${job%%|*}; args=${job#*|}
       (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/$O/prof_$name" -o run \
          -- python "$R/bench.py" $args --no-cpu --no-e2e > "$R/$O/prof_$name.json" 2> "$R/$O/prof_$name.err") \
