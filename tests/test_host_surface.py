@@ -129,7 +129,9 @@ def test_sighup_sigint(tmp_path, exe):
         assert r.p.poll() is None
         assert control(base + 1, b"health\n") == b"health: up\n"
         r.p.send_signal(signal.SIGHUP)
-        time.sleep(0.2)
+        end = time.monotonic() + 5   # the second line (the log is read by a thread of the test)
+        while sum(m == b"on_sighup: sighup received" for _, m in r.lines) < 2 and time.monotonic() < end:
+            time.sleep(0.05)
         assert sum(m == b"on_sighup: sighup received" for _, m in r.lines) == 2
         r.p.send_signal(signal.SIGINT)
         assert r.wait_exit(10) == 0
