@@ -148,7 +148,9 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    if (blockIdx.x < p.nb) {   // scanner of batch blockIdx.x, as in route_kernel
+    uint4 hdr;
+    const uint32_t bi = launch_header_batch(hdr);
+    if (blockIdx.x < hdr.x) {   // scanner of batch blockIdx.x, as in route_kernel
         __builtin_amdgcn_s_setprio(3);
         if (uint64_t *pd = p.b[blockIdx.x].probed_dead)
             for (uint32_t w = tid; w < p.nwords; w += 256) pd[w] = 0ull;
@@ -163,18 +165,15 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         if (tid == 64) arrive(p, blockIdx.x, ep0);
         return;
     }
-    const uint32_t g = blockIdx.x - p.nb;
+    const uint32_t g = blockIdx.x - hdr.x;
     stamp<ABL>(p, tid, g, 8);
-    const uint32_t cls = p.xcd_local ? (g & 7u) : 0u;
-    const uint32_t ci = p.xcd_local ? (g >> 3) : g;
-    uint32_t t;
-    const uint32_t bi = batch_of(p, cls, ci, t);
     if (bi >= kMaxBatches) {
         if (tid == 0) arrive(p, blockIdx.x, __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         return;
     }
     const BatchDesc &bd = p.b[bi];
     const uint32_t nbytes = bd.nbytes;
+    const uint32_t t = (hdr.z ? (g >> 3) : g) - bd.tile0;   // the tile's index in its batch
     const uint32_t T0 = t * 16384u;
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)bd.bytes, (short)0, (int)nbytes, 0x00020000);

@@ -411,14 +411,30 @@ inline int launch_route(DeviceState &ds, const RouteParams &in, hipStream_t stre
         cls_tiles[d.cls] += d.ntiles;
     }
     if (sb > ds.max_tiles) return -EINVAL;
+    // The class table dealt by block index (launch_header_batch in route_kernel.hpp): row r serves the
+    // blocks B = nb + g = r (mod 8); entry = (the first B / 8 past batch j's tiles) << 6 | j. 8+ batches:
+    // row r is class (r - nb) mod 8, whose tile ci runs on block B = nb + 8 ci + class, so B / 8 =
+    // ci + ceil((nb - r) / 8). Fewer: every row holds every batch, tile g on block nb + g, and
+    // g >= end <=> B / 8 >= ceil((end + nb - r) / 8).
     for (int c = 0; c < 8; ++c)
         for (int k = 0; k < kPerClass; ++k) p.cls_tab[c][k] = ~0u;
     {
         int fill[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (uint32_t j = 0; j < p.nb; ++j) {   // j ascending = tile0 ascending within a class
             const BatchDesc &d = p.b[j];
-            if (fill[d.cls] >= kPerClass || d.tile0 + d.ntiles >= (1u << 26)) return -EINVAL;
-            p.cls_tab[d.cls][fill[d.cls]++] = ((d.tile0 + d.ntiles) << 6) | j;
+            const uint32_t end = d.tile0 + d.ntiles;
+            for (uint32_t r = 0; r < 8; ++r) {
+                uint32_t thr;
+                if (xl) {
+                    if (((r + 8u - p.nb % 8u) & 7u) != d.cls) continue;
+                    thr = end + (p.nb - r + 7u) / 8u;   // nb >= 8 > r
+                } else {
+                    const int64_t v = (int64_t)end + p.nb - r;
+                    thr = v <= 0 ? 0u : (uint32_t)((v + 7) / 8);
+                }
+                if (fill[r] >= kPerClass || thr >= (1u << 26)) return -EINVAL;
+                p.cls_tab[r][fill[r]++] = (thr << 6) | j;
+            }
         }
     }
     uint32_t grid_tiles = cls_tiles[0];

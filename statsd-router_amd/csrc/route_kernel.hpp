@@ -232,8 +232,9 @@ struct RouteParams {
     // tile its records' key histogram (shard, or nds = unrouted), key-major per batch at
     // hist[(nds + 1) * sbase + key * ntiles + t], for the packing's sort (mtu_kernel.hpp); null: off
     uint32_t *hist;
-    // per XCD class c, its batches in tile order: (class-local end tile << 6) | batch index;
-    // ~0u after the last (one scalar load finds a tile's batch)
+    // per block residue r = B mod 8, the batches of the tiles those blocks run, in tile order:
+    // (the first B / 8 past the batch's tiles << 6) | batch index; ~0u after the last (one scalar
+    // load, issued with the header's, finds a tile's batch: launch_header_batch)
     uint32_t cls_tab[8][kPerClass];
     BatchDesc b[kMaxBatches];
 };
@@ -1297,17 +1298,38 @@ struct KernelTraits {
 // outstanding global loads.
 __device__ __forceinline__ void wg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// The batch of tile ci of XCD class cls (>= kMaxBatches: a padding block) and the tile's index
-// in it, from one scalar load of the class's row of cls_tab (no chain of dependent loads before
-// the tile's own loads can issue).
-__device__ __forceinline__ uint32_t batch_of(const RouteParams &p, uint32_t cls, uint32_t ci, uint32_t &t) {
-    const uint32_t *row = p.cls_tab[cls];
-    uint32_t k = 0;   // batches of the class that end at or before ci (ends ascend, ~0u pads)
+// A tile workgroup's launch header {nb, total_blocks, xcd_local, nds} and batch, from two scalar
+// loads issued together: the header, and the row of cls_tab for its block index B mod 8, which the
+// host deals by block (route_host.hpp): entry k of row r = (the first B / 8 past batch j's tiles among
+// the blocks B = r (mod 8)) << 6 | j, ascending, ~0u pads. The batch is the row's first entry past
+// B / 8 (63: past the row, a padding block). The tile's class-local index then comes with the batch
+// descriptor (tile0), so that two dependent scalar round trips precede the tile's own loads (the class
+// row indexed by the class, from the header's batch count and mode, was three, and four with the
+// entry re-read by index). The kernels' only argument is the RouteParams, at the kernarg segment's
+// start. Scanner blocks (B < nb) get a batch too and ignore it.
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ uint32_t launch_header_batch(uint4 &hdr) {
+    static_assert(offsetof(RouteParams, nb) == 0 && offsetof(RouteParams, xcd_local) == 8, "header layout");
+    static_assert(sizeof(RouteParams::cls_tab[0]) == 32 && kPerClass == 8, "one s_load_dwordx8 per row");
+    const auto ka = __builtin_amdgcn_kernarg_segment_ptr();
+    const uint32_t roff = (blockIdx.x & 7u) * 32u;
+    u32x8 row;
+    asm volatile("s_load_dwordx4 %0, %2, 0x0\n\t"
+                 "s_load_dwordx8 %1, %2, %3 offset:%4\n\t"
+                 "s_waitcnt lgkmcnt(0)"
+                 : "=&s"(hdr), "=&s"(row)
+                 : "s"(ka), "s"(roff), "i"((int)offsetof(RouteParams, cls_tab)));
+    const uint32_t bx = blockIdx.x >> 3;
+    uint32_t bi = 63u;
+    bool found = false;
 #pragma unroll
-    for (int j = 0; j < kPerClass; ++j) k += ci >= (row[j] >> 6) ? 1u : 0u;
-    if (k >= kPerClass) return 63u;
-    t = ci - (k ? row[k - 1] >> 6 : 0u);
-    return row[k] & 63u;
+    for (int j = 0; j < kPerClass; ++j) {
+        if (!found && bx < (row[j] >> 6)) {
+            bi = row[j] & 63u;
+            found = true;
+        }
+    }
+    return bi;
 }
 
 // One tile's input as loaded into registers: thread tid holds the tile's bytes [64 tid, 64 tid + 64)
@@ -1872,7 +1894,9 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
         if (p.nb > 1000000u) pad[tid] = tid;   // never true: keeps the array
         if (p.nb > 1000000u) p.ctl->pad1 = pad[(tid + 1) & 1023];
     }
-    if (blockIdx.x < p.nb) {   // scanner of batch blockIdx.x (wave 0; no barriers on this path)
+    uint4 hdr;
+    const uint32_t bi = launch_header_batch(hdr);
+    if (blockIdx.x < hdr.x) {   // scanner of batch blockIdx.x (wave 0; no barriers on this path)
         // the scanner is the latency-critical link of every tile's record base: its few
         // instructions go ahead of the co-resident tiles' VALU work
         __builtin_amdgcn_s_setprio(3);
@@ -1896,7 +1920,7 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
         }
         return;
     }
-    const uint32_t g = blockIdx.x - p.nb;   // tile workgroup index within the launch
+    const uint32_t g = blockIdx.x - hdr.x;   // tile workgroup index within the launch
     stamp<ABL>(p, tid, g, 8);
     if ((ABL & ABL_STAMPS) && tid == 0) {   // placement: HW_ID (CU / SH / SE) and XCC_ID
         uint32_t hw;
@@ -1907,22 +1931,22 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     // Launches of 8+ batches keep every batch on one XCD class (blocks b and b + 8 share an XCD):
     // a tile's predecessors then start before it on the same dispatcher, and its scanner (block
     // b, same class) sits beside them.
-    const uint32_t cls = p.xcd_local ? (g & 7u) : 0u;
-    uint32_t ci = p.xcd_local ? (g >> 3) : g;
-    uint32_t t;
-    const uint32_t bi = batch_of(p, cls, ci, t);
     if (bi >= kMaxBatches) {   // padding block of an unbalanced class
         if (tid == 0) arrive(p, blockIdx.x, __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         return;
     }
     // the tile's loads first; the epoch, the scanner's XCD and the power tables (needed only at
     // the count publish and the hash) queue behind them
+    const uint32_t t = (hdr.z ? (g >> 3) : g) - p.b[bi].tile0;   // the tile's index in its batch
     TileIn in;
     tile_issue<BLOCK, ABL>(p, bi, t, in, tid);
     const uint32_t kp = tid < S::kPowWords ? ((const uint32_t *)p.kpow)[tid] : 0u;
-    const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // the scanner granule's load before the epoch's: the epoch's value is wanted at once (a wait for
+    // every load issued before it, vmcnt counts in order), and a granule load issued after that wait
+    // is a whole round trip more before the tile can publish its count (+5 % per C2 launch measured)
     in.sx = (ABL & ABL_AGENT_GRANULES) ? 0ull
                                        : __hip_atomic_load(&p.ctl->scan_xcc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (tid < S::kPowWords) ((uint32_t *)&sm.kp_lo[0])[tid] = kp;   // kp_lo | kp_hi | kp_inv are contiguous
     if (!(ABL & (KV_ALIVE | KV_DEFER1 | KV_DEAD1)) && p.dead && p.dead < p.nds && tid < 4 * (int)kMagicLds) {   // the probe's first reciprocals (probe_shard)
         const uint32_t e = (uint32_t)tid >> 2;   // divisor nds - e >= 1: entries e < nds only
