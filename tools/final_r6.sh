@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-6 final pass on one box, on the shipped build only. Steps (default: all, in this order):
+# Round-6 final pass on one box, on the shipped build only. Steps (default: all, in this order; pmc
+# first so that the bench lines after it report this library's HBM traffic):
 #   tests   every -m gpu test, then __graft_entry__.smoke()
 #   bench   the default bench command three times; C2..C5 lines, all alive and 25 % dead, with route + pack
 #           and two data threads
@@ -14,7 +15,7 @@ O=gpurun_out/$T
 cd "$R" || exit 1
 mkdir -p "$O"
 export TMPDIR=/tmp
-steps=${*:-"tests bench regroup prof pmc c1"}
+steps=${*:-"pmc tests bench regroup prof c1"}
 b() {   # b <name> <bench args...>: one bench line into $O/<name>.json
   local name=$1; shift
   timeout -k 10 300 python bench.py "$@" > "$O/$name.json" 2> "$O/$name.err" || { tail -20 "$O/$name.err"; exit 1; }
@@ -48,6 +49,7 @@ for st in $steps; do
   pmc)
     bash tools/pmc_passes.sh "$O/pmc_c2" --config c2 --steps 100 --no-pack || exit 1
     python tools/pmc_summary.py "$O/pmc_c2" c2 "$O/pmc_summary_c2.json" "$O/bench_traffic_c2.json" --kernel route_kernel || exit 1
+    cp "$O/bench_traffic_c2.json" bench_traffic.json   # this box's copy: the bench steps after it report the traffic
     bash tools/pmc_passes.sh "$O/pmc_c5" --config c5 --steps 100 --no-pack || exit 1
     python tools/pmc_summary.py "$O/pmc_c5" c5 "$O/pmc_summary_c5.json" "$O/bench_traffic_c5.json" --kernel route_chunk_kernel || exit 1 ;;
   c1)
