@@ -186,7 +186,6 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         v[k] = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(rsrc, T0 + (uint32_t)o + 16u * k, 0, 0));
     // unconditional loads (clamped addresses): a load under a lane condition becomes a branch and a
     // wait of its own
-    const uint32_t prevw = t ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, T0 - 4u, 0, 0) : 0x0A000000u;
     constexpr int kKpWords = 2 * (kPowLo + kPowHi);
     const uint32_t kw = ((const uint32_t *)p.kpow)[tid < kKpWords ? tid : kKpWords - 1];
     const uint32_t iw = ((const uint32_t *)p.cpow)[tid < 2 * kCinv ? tid : 2 * kCinv - 1];
@@ -194,6 +193,10 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     // tile's loads: in a tile that some line crosses a chunk boundary of (most C5 tiles), asked for
     // only after the first barrier they were a dependent round trip of their own
     const uint64_t R = p.cpow[kCinv + tid], RI = p.cpow[kCinv + 256 + tid];
+    // the dword before the tile (its last byte: does the tile start a line?), after the tables and at a
+    // clamped address: loaded under `t > 0` it was a branch whose value the compiler waited for at once,
+    // i.e. for every tile load, before the tables' loads were even issued (a round trip more per tile)
+    const uint32_t pw = __builtin_amdgcn_raw_buffer_load_b32(rsrc, T0 ? T0 - 4u : 0u, 0, 0);
     if (T0 + 16384u > nbytes) {
         // the batch's last tile: a piece past the end reads as zeros, but the range check of a 16-byte
         // load that straddles the end is not byte-exact (its bytes before the end can read as zero
@@ -241,7 +244,7 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     }
     if (tid < kKpWords) ((uint32_t *)&sm.kp_lo[0])[tid] = kw;   // kp_lo | kp_hi are contiguous
     if (tid < 2 * kCinv) ((uint32_t *)&sm.kinv[0])[tid] = iw;
-    if (tid == 0) sm.head_nl = (prevw >> 24) == 0x0Au ? 1u : 0u;
+    if (tid == 0) sm.head_nl = t == 0 || (pw >> 24) == 0x0Au ? 1u : 0u;
 
     // ---- line state: three u32 wave scans, the wave totals in LDS ------------------------------
     const uint32_t nrel = nbytes - T0;             // batch bytes from the tile start (> 0)
