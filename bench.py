@@ -170,10 +170,10 @@ def main(argv=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)   # before the process group: its collectives run on this rank's GPU
+    dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", init_method="env://")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
     pkg = importlib.import_module("statsd-router_amd")
     digests = json.load(open(os.path.join(REPO, "tests", "golden", "digests.json")))
 
