@@ -323,11 +323,12 @@ def test_device_many_records_only(pkg, oracle, torch_stream):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("nb", [2, 5, 7, 8, 32])
+@pytest.mark.parametrize("nb", [1, 2, 5, 7, 8, 9, 15, 16, 31, 32])
 def test_device_many_class_tables(pkg, oracle, nb, torch_stream):
-    """Batch lookup table (cls_tab) shapes: 2-7 batches share one class (no XCD-local dealing),
-    8 and 32 are dealt to the 8 XCD classes; sizes differ a lot so classes are unbalanced and
-    padding blocks appear."""
+    """Batch lookup table (cls_tab) shapes: 1-7 batches share one class (no XCD-local dealing; every
+    row of the block-indexed table holds every batch), 8 and more are dealt to the 8 XCD classes (row r
+    = block residue r, its class (r - nb) mod 8, so nb mod 8 shifts the rows); sizes differ a lot so
+    classes are unbalanced and padding blocks appear."""
     import torch
 
     rng = random.Random(1000 + nb)
