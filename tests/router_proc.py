@@ -168,6 +168,28 @@ class HealthServer:
             self.sock = None
 
 
+def wait_control(port: int, timeout=10.0) -> bool:
+    """Until a TCP socket listens on the router's control port (its initialisation, signal handlers
+    included, is done): read passively from /proc/net/tcp, so that the router sees no connection (a
+    fixed sleep after the start flaked on a loaded machine; a probe connection makes the router log
+    while the test may be signalling it, and the reference logs from its signal handler)."""
+    want = ":%04X" % port
+    end = time.monotonic() + timeout
+    while time.monotonic() < end:
+        for path in ("/proc/net/tcp", "/proc/net/tcp6"):
+            try:
+                with open(path) as f:
+                    next(f)
+                    for line in f:
+                        cols = line.split()
+                        if len(cols) > 3 and cols[1].endswith(want) and cols[3] == "0A":   # LISTEN
+                            return True
+            except OSError:
+                pass
+        time.sleep(0.02)
+    return False
+
+
 def control(port: int, request: bytes, timeout=3.0) -> bytes:
     with socket.create_connection(("127.0.0.1", port), timeout=timeout) as s:
         s.sendall(request)

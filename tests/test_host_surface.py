@@ -11,7 +11,7 @@ import time
 
 import pytest
 
-from router_proc import OURS, REFERENCE, HealthServer, Router, config_text, control, free_ports
+from router_proc import OURS, REFERENCE, HealthServer, Router, config_text, control, free_ports, wait_control
 
 BOTH = [OURS] + ([REFERENCE] if os.path.exists(REFERENCE) else [])
 # on a CPU box our data threads cannot open a GPU context: keep the main thread's services running
@@ -78,7 +78,7 @@ def test_control_port_health_replies(tmp_path, exe):
     base = free_ports(4)
     r = Router(exe, config_text(base, base + 1, [(base + 2, base + 3)], log_level=3), str(tmp_path), env=NO_GPU)
     try:
-        time.sleep(0.3)
+        assert wait_control(base + 1)
         assert control(base + 1, b"health\n") == b"health: up\n"
         assert control(base + 1, b"health down\n") == b"health: down\n"
         assert control(base + 1, b"health\n") == b"health: down\n"
@@ -123,16 +123,20 @@ def test_sighup_sigint(tmp_path, exe):
     base = free_ports(4)
     r = Router(exe, config_text(base, base + 1, [(base + 2, base + 3)], log_level=2), str(tmp_path), env=NO_GPU)
     try:
-        time.sleep(0.3)
+        assert wait_control(base + 1)
+        # (both signals before any control request: the reference logs from its signal handler, which is
+        # not safe while its main loop is itself logging, e.g. a control connection's lines)
         r.p.send_signal(signal.SIGHUP)
         assert r.wait_for(lambda lv, m: (lv, m) == ("INFO", b"on_sighup: sighup received"), 5)
         assert r.p.poll() is None
-        assert control(base + 1, b"health\n") == b"health: up\n"
         r.p.send_signal(signal.SIGHUP)
         end = time.monotonic() + 5   # the second line (the log is read by a thread of the test)
         while sum(m == b"on_sighup: sighup received" for _, m in r.lines) < 2 and time.monotonic() < end:
             time.sleep(0.05)
         assert sum(m == b"on_sighup: sighup received" for _, m in r.lines) == 2
+        assert r.p.poll() is None
+        assert control(base + 1, b"health\n") == b"health: up\n"   # still serving
+        time.sleep(0.2)   # its control lines written before the next signal
         r.p.send_signal(signal.SIGINT)
         assert r.wait_exit(10) == 0
         assert ("INFO", b"on_sigint: sigint received") in r.lines
