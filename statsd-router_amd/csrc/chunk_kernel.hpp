@@ -209,6 +209,7 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
     }
     const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t sx = __hip_atomic_load(&p.ctl->scan_xcc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) arrive_count(p, blockIdx.x);   // as route_kernel's tiles (kEarlyArrive)
     if (!(ABL & (KV_ALIVE | KV_DEFER1 | KV_DEAD1)) && p.dead && p.dead < p.nds && tid < 4 * (int)kMagicLds) {   // probe_shard's first reciprocals
         const uint32_t e = (uint32_t)tid >> 2;
         if (e < p.nds) sm.img[(uint32_t)tid * 17 + 16] = ((const uint32_t *)&p.magic[p.nds - e])[tid & 3];
@@ -539,7 +540,7 @@ __global__ __launch_bounds__(256, 7) __attribute__((amdgpu_waves_per_eu(7, 8))) 
         }
     }
     mark_tile_end<ABL>(p, sm.img, bd, t, tid);   // MARK_LDS: the dead shards this tile's probes visited
-    if (tid == 0) arrive(p, blockIdx.x, ep0);
+    if (tid == 0) arrive_last(p, blockIdx.x, ep0);
     prefetch_sink(pf);
     stamp<ABL>(p, tid, g, 9);
 }

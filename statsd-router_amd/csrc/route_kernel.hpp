@@ -1259,8 +1259,10 @@ __device__ uint32_t wait_base(const uint64_t *slot, uint32_t epoch, __amdgpu_buf
 // Arrivals: every block adds itself to a sharded counter (no return value, nothing waits); the
 // last block waits until all have arrived, then resets the counters and advances the epoch.
 // Every block read the epoch before arriving, so none of this launch can see the new one.
-__device__ void arrive(const RouteParams &p, uint32_t blk, uint32_t epoch) {
+__device__ __forceinline__ void arrive_count(const RouteParams &p, uint32_t blk) {
     __hip_atomic_fetch_add(&p.ctl->done[blk & 7u][0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ void arrive_last(const RouteParams &p, uint32_t blk, uint32_t epoch) {
     if (blk != p.total_blocks - 1) return;
     for (uint32_t spin = 0; spin < (1u << 26); ++spin) {
         uint32_t n = 0;
@@ -1284,6 +1286,16 @@ __device__ void arrive(const RouteParams &p, uint32_t blk, uint32_t epoch) {
     }
     __hip_atomic_store(&p.ctl->epoch, epoch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+__device__ void arrive(const RouteParams &p, uint32_t blk, uint32_t epoch) {
+    arrive_count(p, blk);
+    arrive_last(p, blk, epoch);
+}
+// A tile's arrival right after it has read the epoch (the invariant above holds all the same), not
+// at its end: the atomic's round trip then runs under the tile's loads instead of after its last
+// store. Segment-layout launches keep the arrival at the end: their tiles add the layout statistics
+// in their last window, which the last block reads once everyone has arrived.
+template <unsigned ABL>
+constexpr bool kEarlyArrive = (ABL & KV_SEGMENTS) == 0;
 
 template <int BLOCK, unsigned ABL>
 struct KernelTraits {
@@ -1947,6 +1959,7 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
     in.sx = (ABL & ABL_AGENT_GRANULES) ? 0ull
                                        : __hip_atomic_load(&p.ctl->scan_xcc[bi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t ep0 = __hip_atomic_load(&p.ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (kEarlyArrive<ABL> && tid == 0) arrive_count(p, blockIdx.x);
     if (tid < S::kPowWords) ((uint32_t *)&sm.kp_lo[0])[tid] = kp;   // kp_lo | kp_hi | kp_inv are contiguous
     if (!(ABL & (KV_ALIVE | KV_DEFER1 | KV_DEAD1)) && p.dead && p.dead < p.nds && tid < 4 * (int)kMagicLds) {   // the probe's first reciprocals (probe_shard)
         const uint32_t e = (uint32_t)tid >> 2;   // divisor nds - e >= 1: entries e < nds only
@@ -1970,7 +1983,10 @@ __attribute__((amdgpu_waves_per_eu((KernelTraits<BLOCK, ABL>::kMinWavesPerSimd),
         if ((uint32_t)tid <= p.nds)
             p.hist[(size_t)(p.nds + 1) * bd.sbase + (size_t)tid * bd.ntiles + t] = sm.hist[tid];
     }
-    if (tid == 0) arrive(p, blockIdx.x, ep0);
+    if (tid == 0) {
+        if (kEarlyArrive<ABL>) arrive_last(p, blockIdx.x, ep0);
+        else arrive(p, blockIdx.x, ep0);
+    }
     stamp<ABL>(p, tid, g, 9);
 }
 
